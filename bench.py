@@ -1,0 +1,231 @@
+"""Benchmark: RGBD keypoint inference throughput (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--precision fp16]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = one KeypointCNN forward (perseus/detector/models.py:34-40) over a batch of 64
+synthetic 256x256 RGBD frames already resident in HBM (BASELINE.json configs[1]).  At
+N > 1 each rank runs its own frame shard (weak scaling, weights replicated) and the
+keypoints of the whole run are all-gathered once over RCCL at the end of the timed
+region (configs[2]).  Rank 0 prints one JSON line; see DESIGN.md "measurement".
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MFMA_FP16_DENSE_PEAK = 2.5e15  # MI355X_MICROARCH.md: ~2.5 PF dense fp16/bf16
+MFMA_FP32_PEAK = 157.3e12      # f32-input MFMA peak (= vector f32 rate)
+HBM_PEAK = 8.0e12
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch", type=int, default=64)
+    p.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--profile-passes", type=int, default=5)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from perseus_amd import synth
+    from perseus_amd.detector import KeypointCNN
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    B = args.batch
+    state = synth.synthetic_state_dict(args.seed)
+    model = KeypointCNN(num_channels=4, precision=args.precision)
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
+    model.eval()
+    # this rank's frame shard, resident in HBM before timing
+    x_host = synth.synthetic_frames(args.seed, B, first=rank * B)
+    x = torch.from_numpy(x_host).to(dev)
+    model.reserve(B, dev)
+    kp = torch.empty((args.steps, B, 16), dtype=torch.float32, device=dev)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            model(x)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            kp[i] = model(x)
+        if world > 1:  # one all-gather of all keypoints (configs[2])
+            gathered = [torch.empty_like(kp) for _ in range(world)]
+            dist.all_gather(gathered, kp)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames = world * B * args.steps
+    value = frames / elapsed
+    flops_frame = model.flops_per_frame()
+
+    # per-kernel HIP-event timing of the same forward on the same stream
+    prof_acc = {}
+    for _ in range(args.profile_passes):
+        prof, _ = model.profile(x)
+        for idx, (name, ms) in enumerate(prof):
+            prof_acc.setdefault((idx, name), []).append(ms)
+    per_launch = [(idx, name, statistics.median(v)) for (idx, name), v in sorted(prof_acc.items())]
+
+    line = None
+    if rank == 0:
+        roof = roofline(per_launch, B, args.precision)
+        px = px_error(model, x_host, state, dev)
+        cpu = None if (world > 1 or args.no_cpu_baseline) else cpu_baseline(state, x_host)
+        per_gpu = value / world
+        line = {
+            "metric": "RGBD frames/sec/GPU (256x256, batch 64); keypoint px-L2 vs CPU ref",
+            "value": round(value, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (seeded RGBD frames + seeded ResNet-18 weights; no dataset/checkpoint offline)",
+            "config": {"workload": "keypointcnn_rgbd256_b64_forward", "per_gpu_batch": B, "global_batch": B * world,
+                       "H": 256, "W": 256, "channels": 4, "precision": args.precision,
+                       "inputs": "device-resident f32 NCHW", "parallelism": f"dp{world}"},
+            "frames_per_s_per_gpu": round(per_gpu, 1),
+            "e2e_mfma_roofline_frac": round(per_gpu * flops_frame /
+                                            (MFMA_FP16_DENSE_PEAK if args.precision == "fp16" else MFMA_FP32_PEAK), 4),
+            "roofline": roof,
+            "px_l2": px,
+            "cpu_baseline": cpu,
+            "kernels_ms": {f"{i:02d}_{n}": round(ms, 4) for i, n, ms in per_launch},
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return line
+
+
+def conv_flops(B):
+    """Algorithmic FLOPs per launch, in forward order (matches pa_detector_profile)."""
+    fl = [2.0 * B * 128 * 128 * 64 * 49 * 4, 0.0]  # stem (true K = 196), maxpool
+    hw, cin = 64, 64
+    for li, cout in enumerate((64, 128, 256, 512)):
+        for bi in range(2):
+            s = 2 if (li > 0 and bi == 0) else 1
+            ho = hw // s
+            c_in = cin if bi == 0 else cout
+            fl.append(2.0 * B * ho * ho * cout * 9 * c_in)          # conv1
+            if bi == 0 and li > 0:
+                fl.append(2.0 * B * ho * ho * cout * c_in)          # downsample
+            fl.append(2.0 * B * ho * ho * cout * 9 * cout)          # conv2
+            hw = ho
+        cin = cout
+    fl.append(2.0 * B * 512 * 16)
+    return fl
+
+
+def roofline(per_launch, B, precision):
+    fl = conv_flops(B)
+    if len(fl) != len(per_launch):
+        return None
+    groups = {}
+    for (idx, name, ms), f in zip(per_launch, fl):
+        g = groups.setdefault(name, [0.0, 0.0, 0])
+        g[0] += ms
+        g[1] += f
+        g[2] += 1
+    name, (ms, f, n) = max(groups.items(), key=lambda kv: kv[1][0])
+    peak = MFMA_FP16_DENSE_PEAK if precision == "fp16" else MFMA_FP32_PEAK
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            with open(tf) as fh:
+                traffic = json.load(fh).get(precision, {}).get(name)
+        except Exception:
+            traffic = None
+    if f == 0:  # bandwidth kernel dominant (maxpool)
+        return {"kernel": name, "bound": "hbm", "achieved": None, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": None, "traffic": traffic, "launches": n, "avg_ms": ms / n}
+    achieved = f / (ms * 1e-3)
+    return {"kernel": name, "bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": peak / 1e12,
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic, "launches": n,
+            "avg_ms": round(ms / n, 5), "flops_per_launch": f / n}
+
+
+def px_error(model, x_host, state, dev, nframes=8):
+    import numpy as np
+    import torch
+
+    from oracle import resnet_ref as R
+
+    xs = x_host[:nframes]
+    y = model(torch.from_numpy(xs).to(dev)).cpu().numpy()
+    yref = R.run(state, xs, torch.float32)
+    d = (np.abs(y - yref) * 127.5).reshape(len(xs), -1, 2)
+    l2 = np.sqrt((d ** 2).sum(-1))
+    return {"max": float(l2.max()), "mean": float(l2.mean()), "frames": int(len(xs)),
+            "vs": "reference-equivalent torch CPU f32 forward (oracle/resnet_ref.py)"}
+
+
+def cpu_baseline(state, x_host, warm=2, iters=5):
+    import numpy as np
+    import torch
+
+    from oracle import resnet_ref as R
+
+    threads = torch.get_num_threads()
+    sd = R.to_torch(state, torch.float32)
+    x = torch.from_numpy(np.ascontiguousarray(x_host))
+    times = []
+    with torch.no_grad():
+        for i in range(warm + iters):
+            t0 = time.perf_counter()
+            R.forward(sd, x)
+            if i >= warm:
+                times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(x.shape[0] / med, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{iters} timed (+{warm} warm-up) torch-CPU f32 forwards of the same batch of {x.shape[0]} "
+                      f"frames, median; threads=torch.get_num_threads()"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+/*
+ * perseus_amd — C ABI of the MI355X keypoint-inference path (libperseus_amd.so).
+ *
+ * Plain pointers and sizes only; every array argument named *_dev is a device
+ * pointer (hipMalloc / torch CUDA tensor storage) owned by the caller, every
+ * `stream` is a hipStream_t passed as void* (NULL = default stream).  All entry
+ * points return 0 on success and a negative PA_E* code on failure, with a
+ * thread-local message in pa_last_error().  Nothing here synchronises the
+ * stream; results are ready when the caller's stream work completes.
+ *
+ * Reference interfaces replaced (paths relative to pculbertson/perseus):
+ *   detector  perseus/detector/models.py:6-40   KeypointCNN.__init__/forward
+ *             perseus/detector/validate.py:92-98 ckpt load ("module." strip) + eval
+ *   factors   perseus/smoother/factors.py:54-142  PoseDynamicsFactor.error_func
+ *             perseus/smoother/factors.py:160-171 ConstantVelocityFactor.error_func
+ *             perseus/smoother/factors.py:216-275 KeypointProjectionFactor.error_func
+ */
+#ifndef PERSEUS_AMD_H
+#define PERSEUS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PA_OK 0
+#define PA_EINVAL -1   /* bad argument (shape, size, null pointer)           */
+#define PA_EHIP -2     /* HIP runtime error (message has hipGetErrorString)   */
+#define PA_ENOMEM -3   /* device allocation failed                            */
+
+#define PA_PREC_FP16 0 /* fp16 NHWC activations/weights, fp32 MFMA accumulate */
+#define PA_PREC_FP32 1 /* fp32 NHWC, exact-f32 MFMA (parity mode)             */
+
+#define PA_VEL_WORLD 0 /* factors.py:41 vel_frame="world" */
+#define PA_VEL_BODY 1  /* vel_frame="body"                */
+
+const char* pa_last_error(void);
+const char* pa_version(void);
+
+/* ------------------------------------------------------------------ detector */
+typedef struct pa_detector pa_detector;
+
+/* Replaces KeypointCNN(n_keypoints, num_channels, H, W) + load_state_dict + eval()
+ * (models.py:9-32, validate.py:92-98).
+ * weights: HOST f32 blob = the state-dict float tensors in torchvision resnet18
+ * order with the "resnet." prefix and without the 20 num_batches_tracked
+ * counters (conv1.weight [64,C,7,7]; bn1.{weight,bias,running_mean,running_var};
+ * layer1.0.conv1.weight ... ; fc.weight [2K,512]; fc.bias [2K]) — 102 tensors,
+ * nbytes must equal the sum of their sizes.  BatchNorm (eps 1e-5) is folded and
+ * weights are packed for the GPU here, once.  Only H = W = 256 and
+ * 1 <= in_ch <= 4 are supported (the trained configurations). */
+int pa_detector_create(const float* weights, size_t nbytes, int in_ch, int n_kp, int H, int W,
+                       pa_detector** out);
+void pa_detector_destroy(pa_detector* d);
+
+/* Pre-size the activation workspace for batches up to max_batch (allocation is
+ * otherwise done lazily on the first larger forward; it is never done inside a
+ * captured graph). */
+int pa_detector_reserve(pa_detector* d, int max_batch);
+
+/* PA_PREC_FP16 (default) or PA_PREC_FP32. */
+int pa_detector_set_precision(pa_detector* d, int precision);
+
+/* Replaces KeypointCNN.forward (models.py:34-40): x (B,C,H,W) f32 NCHW contiguous
+ * on the device -> y (B, 2K) f32, y[:,2k] = x_k, y[:,2k+1] = y_k in [-1,1]
+ * normalized image coordinates.  B = 0 is a no-op. */
+int pa_detector_forward(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream);
+
+/* Same forward with a HIP event after every kernel: writes up to max_n per-kernel
+ * durations (ms) into ms_out and their names into names_out (may be NULL), returns
+ * the number of kernels or <0.  Synchronises the stream (diagnostics only). */
+int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream,
+                        float* ms_out, const char** names_out, int max_n);
+
+/* Algorithmic FLOPs of one frame's forward (2 x MAC over the 20 convs + fc). */
+double pa_detector_flops_per_frame(const pa_detector* d);
+
+/* Fused preprocessing (streaming.py:59-82, augmentations.py:128-169
+ * val mode): RGB uint8 (B,Hs,Ws,3, BGR if bgr) + f32 depth metres (B,Hs,Ws),
+ * centre crop to H x W, rgb/255, depth nan/inf -> 0, depth/0.035, then the
+ * deterministic near/far clip (scaled depth < near or > far -> 0; pass near<0 /
+ * far<0 to skip) -> x (B,4,H,W) f32 NCHW on the device. */
+int pa_preprocess_rgbd(const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws, int bgr,
+                       float near_m, float far_m, int H, int W, float* x_dev, void* stream);
+
+/* Keypoint post-processing on device (validate.py:130-153): px = (n+1)(S-1)/2 into
+ * px_dev (B,K,2); if target_dev != NULL (B,2K normalized), SmoothL1(beta=1) per
+ * element into loss_dev (B,2K). */
+int pa_keypoints_postprocess(const float* y_dev, const float* target_dev, int B, int n_kp, int H, int W,
+                             float* px_dev, float* loss_dev, void* stream);
+
+/* ------------------------------------------------------------------- factors */
+/* Pose encoding: 12 f64 per pose = R row-major (9) then t (3).  Jacobians are
+ * column-major per factor (Eigen/GTSAM order), tangent order [omega; v].
+ * inv_sigma (may be NULL): per-dimension 1/sigma of a diagonal noise model; when
+ * given, r and every J are whitened in place (A = J/sigma, r_w = r/sigma) and
+ * err_dev[i] = 0.5 * ||r_w||^2 (GTSAM NoiseModelFactor::error). err_dev may be NULL. */
+
+/* KeypointProjectionFactor (factors.py:216-275): r = pi(K, Tcam^-1 Tbody p_b) - z,
+ * J = d r / d Tbody (2x6).  K = (fx, fy, s, u0, v0); k_stride / tcam_stride = 0
+ * share one K / camera pose across factors, 5 / 12 give one per factor; tcam_dev
+ * NULL = identity camera (factors.py:211).  status[i] = 1 on cheirality (point
+ * behind the camera: GTSAM CheiralityException), r and J then hold NaN. */
+int pa_proj_linearize(int n, const double* tbody_dev, const double* pb_dev, const double* z_dev,
+                      const double* k_dev, int k_stride, const double* tcam_dev, int tcam_stride,
+                      const double* inv_sigma_dev, double* r_dev, double* j_dev, double* err_dev,
+                      int32_t* status_dev, void* stream);
+
+/* PoseDynamicsFactor (factors.py:54-142): r = Log((T1 Exp(dt[w; v_b]))^-1 T2),
+ * v_b = R1^T v if vel_frame == PA_VEL_WORLD.  J0 6x6 (pose1), J1 6x3 (ang_vel1),
+ * J2 6x3 (vel1), J3 6x6 (pose2); any J pointer may be NULL (error-only). */
+int pa_dyn_linearize(int n, const double* t1_dev, const double* w_dev, const double* v_dev,
+                     const double* t2_dev, double dt, int vel_frame, const double* inv_sigma_dev,
+                     double* r_dev, double* j0_dev, double* j1_dev, double* j2_dev, double* j3_dev,
+                     double* err_dev, void* stream);
+
+/* ConstantVelocityFactor (factors.py:160-171): r = v2 - v1, J0 = -I3, J1 = I3. */
+int pa_cv_linearize(int n, const double* v1_dev, const double* v2_dev, const double* inv_sigma_dev,
+                    double* r_dev, double* j0_dev, double* j1_dev, double* err_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PERSEUS_AMD_H */

@@ -1,0 +1,97 @@
+"""ctypes binding of libperseus_amd.so (the C ABI in include/perseus_amd.h).
+
+The library is the product: there is no fallback.  If it is missing or fails to
+load, `lib()` raises; build it with `python -m perseus_amd.build`.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import build as _build
+
+_LIB = None
+
+c_double_p = C.POINTER(C.c_double)
+c_float_p = C.POINTER(C.c_float)
+
+
+class PerseusError(RuntimeError):
+    pass
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "pa_last_error": (C.c_char_p, []),
+    "pa_version": (C.c_char_p, []),
+    "pa_detector_create": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.POINTER(C.c_void_p)]),
+    "pa_detector_destroy": (None, [C.c_void_p]),
+    "pa_detector_reserve": (C.c_int, [C.c_void_p, C.c_int]),
+    "pa_detector_set_precision": (C.c_int, [C.c_void_p, C.c_int]),
+    "pa_detector_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "pa_detector_profile": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_int]),
+    "pa_detector_flops_per_frame": (C.c_double, [C.c_void_p]),
+    "pa_preprocess_rgbd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_float, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
+    "pa_keypoints_postprocess": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pa_proj_linearize": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                    C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p]),
+    "pa_dyn_linearize": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
+                                   C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pa_cv_linearize": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p]),
+}
+
+PREC_FP16 = 0
+PREC_FP32 = 1
+VEL_WORLD = 0
+VEL_BODY = 1
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def lib(build_if_missing: bool = True):
+    """Load (and on first use, if absent and a compiler exists, build) the library."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = _build.LIB
+    if not os.path.exists(path) and build_if_missing:
+        _build.build()
+    if not os.path.exists(path):
+        raise PerseusError(f"{path} not found: run `python -m perseus_amd.build`")
+    L = C.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str = "") -> int:
+    if rc < 0:
+        msg = lib().pa_last_error().decode(errors="replace")
+        raise PerseusError(f"{what}: {msg} (code {rc})" if what else f"{msg} (code {rc})")
+    return rc
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_of(device) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

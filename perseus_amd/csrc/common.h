@@ -1,0 +1,44 @@
+// Shared helpers for the perseus_amd HIP library (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <cstdio>
+#include <string>
+
+#include "../../include/perseus_amd.h"
+
+namespace pa {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+void set_error(const char* fmt, ...);
+
+#define PA_HIP(call)                                                               \
+  do {                                                                             \
+    hipError_t _e = (call);                                                        \
+    if (_e != hipSuccess) {                                                        \
+      ::pa::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call, hipGetErrorString(_e)); \
+      return PA_EHIP;                                                              \
+    }                                                                              \
+  } while (0)
+
+#define PA_CHECK(cond, ...)          \
+  do {                               \
+    if (!(cond)) {                   \
+      ::pa::set_error(__VA_ARGS__);  \
+      return PA_EINVAL;              \
+    }                                \
+  } while (0)
+
+#define PA_LAUNCH_CHECK()                                                              \
+  do {                                                                                 \
+    hipError_t _e = hipGetLastError();                                                 \
+    if (_e != hipSuccess) {                                                            \
+      ::pa::set_error("%s:%d launch: %s", __FILE__, __LINE__, hipGetErrorString(_e)); \
+      return PA_EHIP;                                                                  \
+    }                                                                                  \
+  } while (0)
+
+}  // namespace pa

@@ -1,0 +1,37 @@
+// Launchers for the detector kernels (conv.hip).  Precision is a template
+// parameter everywhere: T = _Float16 (fast path) or float (parity path).
+#pragma once
+#include "common.h"
+
+namespace pa {
+
+enum { EPI_RELU = 1, EPI_RES = 2 };
+
+struct ConvArgs {
+  const void* in;     // NHWC [B][Hin][Win][Cin]
+  const void* w;      // [Cout][KS][KS][Cin], BatchNorm folded
+  const float* bias;  // [Cout], BatchNorm folded
+  const void* res;    // NHWC [B][Hout][Wout][Cout] or nullptr
+  void* out;          // NHWC [B][Hout][Wout][Cout]
+  int B, Hin, Win, Cin, Hout, Wout, Cout, stride, pad, epi, M;
+};
+
+template <typename T>
+int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);
+
+template <typename T>
+int launch_stem(const float* x, int B, int Cin, const T* w, const float* bias, T* out, hipStream_t s);
+
+template <typename T>
+int launch_maxpool(const T* in, int B, int H, int W, int C, T* out, hipStream_t s);
+
+template <typename T>
+int launch_head(const T* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
+                hipStream_t s);
+
+int launch_preprocess(const uint8_t* rgb, const float* depth, int B, int Hs, int Ws, int bgr, float near_m,
+                      float far_m, int H, int W, float* x, hipStream_t s);
+int launch_postprocess(const float* y, const float* target, int B, int n_kp, int H, int W, float* px,
+                       float* loss, hipStream_t s);
+
+}  // namespace pa

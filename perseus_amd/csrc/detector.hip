@@ -1,0 +1,405 @@
+// Host side of the detector: state-dict blob parsing, BatchNorm folding, weight
+// packing for the GPU kernels, workspace management and the forward schedule.
+// Exposes the C ABI declared in include/perseus_amd.h.
+//
+// Reference: perseus/detector/models.py:6-40 (KeypointCNN), torchvision
+// resnet18 layer graph (stem, 4 stages x 2 BasicBlocks, avgpool, fc).
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "conv.h"
+
+namespace pa {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+struct ConvL {
+  int cin, cout, ks, stride, pad;
+  size_t w_off;  // element offset into the packed weight arrays
+  size_t b_off;  // element offset into the bias array
+};
+
+struct Block {
+  int conv1, conv2, ds;  // indices into convs; ds = -1 when identity
+};
+
+}  // namespace pa
+
+struct pa_detector {
+  int in_ch = 4, n_kp = 8, H = 256, W = 256, prec = PA_PREC_FP16;
+  std::vector<pa::ConvL> convs;  // convs[0] = stem
+  std::vector<pa::Block> blocks;
+  _Float16* w16 = nullptr;
+  float* w32 = nullptr;
+  float* bias = nullptr;
+  float* fcw = nullptr;
+  float* fcb = nullptr;
+  char* ws = nullptr;
+  size_t ws_bytes = 0;
+  double flops_per_frame = 0;
+  int device = 0;
+};
+
+namespace pa {
+
+// Parse + fold + pack.  Returns PA_OK or an error code.
+static int build(pa_detector* d, const float* blob, size_t nfloats) {
+  size_t pos = 0;
+  auto take = [&](size_t n) -> const float* {
+    if (pos + n > nfloats) return nullptr;
+    const float* p = blob + pos;
+    pos += n;
+    return p;
+  };
+  std::vector<_Float16> h16;
+  std::vector<float> h32, hb;
+
+  // conv weight + BN -> packed [cout][ks][ks][cin] (stem: [64][7][32])
+  auto add_conv = [&](int cin, int cout, int ks, int stride, int pad, bool stem) -> int {
+    const float* w = take((size_t)cout * cin * ks * ks);
+    const float* g = take(cout);
+    const float* b = take(cout);
+    const float* mu = take(cout);
+    const float* var = take(cout);
+    if (!w || !g || !b || !mu || !var) return -1;
+    ConvL L{cin, cout, ks, stride, pad, h32.size(), hb.size()};
+    const int K = stem ? 7 * 32 : ks * ks * cin;
+    std::vector<float> packed((size_t)cout * K, 0.f);
+    for (int co = 0; co < cout; ++co) {
+      const double scale = (double)g[co] / std::sqrt((double)var[co] + 1e-5);
+      hb.push_back((float)((double)b[co] - (double)mu[co] * scale));
+      for (int ci = 0; ci < cin; ++ci)
+        for (int kr = 0; kr < ks; ++kr)
+          for (int kc = 0; kc < ks; ++kc) {
+            const double v = (double)w[(((size_t)co * cin + ci) * ks + kr) * ks + kc] * scale;
+            size_t k = stem ? (size_t)kr * 32 + kc * 4 + ci : ((size_t)kr * ks + kc) * cin + ci;
+            packed[(size_t)co * K + k] = (float)v;
+          }
+    }
+    for (float v : packed) {
+      h32.push_back(v);
+      h16.push_back((_Float16)v);
+    }
+    d->convs.push_back(L);
+    const double taps = stem ? 7.0 * 7.0 * cin : (double)ks * ks * cin;
+    (void)taps;
+    return (int)d->convs.size() - 1;
+  };
+
+  if (add_conv(d->in_ch, 64, 7, 2, 3, true) < 0) return -1;
+  int cin = 64;
+  const int couts[4] = {64, 128, 256, 512};
+  for (int li = 0; li < 4; ++li) {
+    for (int bi = 0; bi < 2; ++bi) {
+      const int cout = couts[li];
+      const int stride = (li > 0 && bi == 0) ? 2 : 1;
+      const int bcin = bi == 0 ? cin : cout;
+      Block blk;
+      blk.conv1 = add_conv(bcin, cout, 3, stride, 1, false);
+      blk.conv2 = add_conv(cout, cout, 3, 1, 1, false);
+      blk.ds = -1;
+      if (blk.conv1 < 0 || blk.conv2 < 0) return -1;
+      if (bi == 0 && (stride != 1 || bcin != cout)) {
+        blk.ds = add_conv(bcin, cout, 1, stride, 0, false);
+        if (blk.ds < 0) return -1;
+      }
+      d->blocks.push_back(blk);
+    }
+    cin = couts[li];
+  }
+  const int nout = 2 * d->n_kp;
+  const float* fw = take((size_t)nout * 512);
+  const float* fb = take(nout);
+  if (!fw || !fb) return -1;
+  if (pos != nfloats) return -2;
+
+  // algorithmic FLOPs (2 x MAC; stem at its true K = 49*Cin)
+  const int hw_in[4] = {64, 64, 32, 16};
+  (void)hw_in;
+  double fl = 2.0 * 128 * 128 * 64 * 49.0 * d->in_ch;
+  int hw = 64;
+  for (const Block& b : d->blocks) {
+    const ConvL& c1 = d->convs[b.conv1];
+    const int ho = hw / c1.stride;
+    fl += 2.0 * ho * ho * c1.cout * 9.0 * c1.cin;
+    fl += 2.0 * ho * ho * c1.cout * 9.0 * c1.cout;
+    if (b.ds >= 0) fl += 2.0 * ho * ho * c1.cout * (double)c1.cin;
+    hw = ho;
+  }
+  fl += 2.0 * 512 * nout;
+  d->flops_per_frame = fl;
+
+  PA_HIP(hipMalloc(&d->w16, h16.size() * sizeof(_Float16)));
+  PA_HIP(hipMalloc(&d->w32, h32.size() * sizeof(float)));
+  PA_HIP(hipMalloc(&d->bias, hb.size() * sizeof(float)));
+  PA_HIP(hipMalloc(&d->fcw, (size_t)nout * 512 * sizeof(float)));
+  PA_HIP(hipMalloc(&d->fcb, (size_t)nout * sizeof(float)));
+  PA_HIP(hipMemcpy(d->w16, h16.data(), h16.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(d->w32, h32.data(), h32.size() * sizeof(float), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(d->bias, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(d->fcw, fw, (size_t)nout * 512 * sizeof(float), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(d->fcb, fb, (size_t)nout * sizeof(float), hipMemcpyHostToDevice));
+  return PA_OK;
+}
+
+static size_t ws_need(int B, int prec) {
+  const size_t es = prec == PA_PREC_FP32 ? 4 : 2;
+  const size_t stem = (size_t)B * 128 * 128 * 64;
+  const size_t act = (size_t)B * 64 * 64 * 64;
+  return (stem + 3 * act) * es + 1024;
+}
+
+static int ensure_ws(pa_detector* d, int B) {
+  const size_t need = ws_need(B, d->prec);
+  if (need <= d->ws_bytes) return PA_OK;
+  if (d->ws) {
+    PA_HIP(hipFree(d->ws));
+    d->ws = nullptr;
+    d->ws_bytes = 0;
+  }
+  if (hipMalloc(&d->ws, need) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("workspace: hipMalloc(%zu) failed", need);
+    return PA_ENOMEM;
+  }
+  d->ws_bytes = need;
+  return PA_OK;
+}
+
+struct Prof {
+  std::vector<hipEvent_t> ev;
+  std::vector<const char*> names;
+  hipStream_t s;
+  void mark(const char* name) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    hipEventRecord(e, s);
+    ev.push_back(e);
+    names.push_back(name);
+  }
+};
+
+#define PA_TRY(x)                \
+  do {                           \
+    int _rc = (x);               \
+    if (_rc != PA_OK) return _rc; \
+  } while (0)
+
+template <typename T>
+static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof) {
+  const T* wts = std::is_same<T, float>::value ? (const T*)d->w32 : (const T*)d->w16;
+  T* S = reinterpret_cast<T*>(d->ws);
+  const size_t stem_el = (size_t)B * 128 * 128 * 64;
+  const size_t act_el = (size_t)B * 64 * 64 * 64;
+  T* X = S + stem_el;
+  T* Tb = X + act_el;
+  T* D = Tb + act_el;
+  if (prof) prof->mark("start");
+  const ConvL& st = d->convs[0];
+  PA_TRY(launch_stem<T>(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, S, s));
+  if (prof) prof->mark("stem_conv7x7");
+  PA_TRY(launch_maxpool<T>(S, B, 128, 128, 64, X, s));
+  if (prof) prof->mark("maxpool");
+  int hw = 64;
+  for (const Block& b : d->blocks) {
+    const ConvL& c1 = d->convs[b.conv1];
+    const ConvL& c2 = d->convs[b.conv2];
+    const int ho = hw / c1.stride;
+    const char* kn = nullptr;
+    ConvArgs a{};
+    a.B = B;
+    a.Hin = hw;
+    a.Win = hw;
+    a.Hout = ho;
+    a.Wout = ho;
+    a.M = B * ho * ho;
+    // conv1 + bn1 + relu
+    a.in = X;
+    a.w = wts + c1.w_off;
+    a.bias = d->bias + c1.b_off;
+    a.res = nullptr;
+    a.out = Tb;
+    a.Cin = c1.cin;
+    a.Cout = c1.cout;
+    a.stride = c1.stride;
+    a.pad = 1;
+    a.epi = EPI_RELU;
+    PA_TRY(launch_conv<T>(a, 3, s, &kn));
+    if (prof) prof->mark(kn);
+    const T* res = X;
+    T* out = X;  // identity block: residual add in place (same element, same thread)
+    if (b.ds >= 0) {
+      const ConvL& cd = d->convs[b.ds];
+      ConvArgs dsa = a;
+      dsa.w = wts + cd.w_off;
+      dsa.bias = d->bias + cd.b_off;
+      dsa.out = D;
+      dsa.pad = 0;
+      dsa.epi = 0;
+      PA_TRY(launch_conv<T>(dsa, 1, s, &kn));
+      if (prof) prof->mark(kn);
+      res = D;
+      out = D;
+    }
+    // conv2 + bn2 + residual + relu
+    ConvArgs b2{};
+    b2.B = B;
+    b2.Hin = ho;
+    b2.Win = ho;
+    b2.Hout = ho;
+    b2.Wout = ho;
+    b2.M = B * ho * ho;
+    b2.in = Tb;
+    b2.w = wts + c2.w_off;
+    b2.bias = d->bias + c2.b_off;
+    b2.res = res;
+    b2.out = out;
+    b2.Cin = c2.cin;
+    b2.Cout = c2.cout;
+    b2.stride = 1;
+    b2.pad = 1;
+    b2.epi = EPI_RELU | EPI_RES;
+    PA_TRY(launch_conv<T>(b2, 3, s, &kn));
+    if (prof) prof->mark(kn);
+    if (b.ds >= 0) std::swap(X, D);
+    hw = ho;
+  }
+  PA_TRY(launch_head<T>(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s));
+  if (prof) prof->mark("avgpool_fc");
+  return PA_OK;
+}
+
+static int forward(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof) {
+  PA_CHECK(d, "null detector");
+  PA_CHECK(B >= 0, "batch %d", B);
+  if (B == 0) return PA_OK;
+  PA_CHECK(x && y, "null input/output pointer");
+  PA_TRY(ensure_ws(d, B));
+  return d->prec == PA_PREC_FP32 ? forward_t<float>(d, x, B, y, s, prof) : forward_t<_Float16>(d, x, B, y, s, prof);
+}
+
+}  // namespace pa
+
+extern "C" {
+
+const char* pa_last_error(void) { return pa::g_err.c_str(); }
+const char* pa_version(void) { return "perseus_amd 0.1 gfx950"; }
+
+int pa_detector_create(const float* weights, size_t nbytes, int in_ch, int n_kp, int H, int W, pa_detector** out) {
+  PA_CHECK(out, "null out");
+  *out = nullptr;
+  PA_CHECK(weights, "null weights");
+  PA_CHECK(H == 256 && W == 256, "only 256x256 inputs are supported (got %dx%d)", H, W);
+  PA_CHECK(in_ch >= 1 && in_ch <= 4, "in_ch %d not in [1,4]", in_ch);
+  PA_CHECK(n_kp >= 1 && n_kp <= 16, "n_kp %d not in [1,16]", n_kp);
+  PA_CHECK(nbytes % 4 == 0, "nbytes %zu not a multiple of 4", nbytes);
+  pa_detector* d = new pa_detector();
+  d->in_ch = in_ch;
+  d->n_kp = n_kp;
+  d->H = H;
+  d->W = W;
+  if (hipGetDevice(&d->device) != hipSuccess) {
+    delete d;
+    pa::set_error("hipGetDevice failed (no GPU?)");
+    return PA_EHIP;
+  }
+  int rc = pa::build(d, weights, nbytes / 4);
+  if (rc != PA_OK) {
+    if (rc == -1 || rc == -2) {
+      pa::set_error("weight blob size mismatch: %zu bytes for in_ch=%d n_kp=%d", nbytes, in_ch, n_kp);
+      rc = PA_EINVAL;
+    }
+    pa_detector_destroy(d);
+    return rc;
+  }
+  *out = d;
+  return PA_OK;
+}
+
+void pa_detector_destroy(pa_detector* d) {
+  if (!d) return;
+  hipFree(d->w16);
+  hipFree(d->w32);
+  hipFree(d->bias);
+  hipFree(d->fcw);
+  hipFree(d->fcb);
+  if (d->ws) hipFree(d->ws);
+  delete d;
+}
+
+int pa_detector_reserve(pa_detector* d, int max_batch) {
+  PA_CHECK(d && max_batch >= 0, "bad arguments");
+  return pa::ensure_ws(d, max_batch);
+}
+
+int pa_detector_set_precision(pa_detector* d, int precision) {
+  PA_CHECK(d, "null detector");
+  PA_CHECK(precision == PA_PREC_FP16 || precision == PA_PREC_FP32, "precision %d", precision);
+  if (precision != d->prec) {
+    // keep the same batch capacity for the new element size
+    const size_t old = d->ws_bytes;
+    int bcap = 0;
+    while (bcap < (1 << 20) && pa::ws_need(bcap + 1, d->prec) <= old) ++bcap;
+    d->prec = precision;
+    if (bcap > 0) return pa::ensure_ws(d, bcap);
+  }
+  return PA_OK;
+}
+
+int pa_detector_forward(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream) {
+  return pa::forward(d, x_dev, B, y_dev, (hipStream_t)stream, nullptr);
+}
+
+int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream, float* ms_out,
+                        const char** names_out, int max_n) {
+  pa::Prof p;
+  p.s = (hipStream_t)stream;
+  int rc = pa::forward(d, x_dev, B, y_dev, p.s, &p);
+  if (rc == PA_OK && hipStreamSynchronize(p.s) != hipSuccess) {
+    pa::set_error("profile: stream sync failed");
+    rc = PA_EHIP;
+  }
+  int n = 0;
+  if (rc == PA_OK) {
+    for (size_t i = 1; i < p.ev.size() && n < max_n; ++i, ++n) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, p.ev[i - 1], p.ev[i]);
+      if (ms_out) ms_out[n] = ms;
+      if (names_out) names_out[n] = p.names[i];
+    }
+  }
+  for (hipEvent_t e : p.ev) hipEventDestroy(e);
+  return rc == PA_OK ? n : rc;
+}
+
+double pa_detector_flops_per_frame(const pa_detector* d) { return d ? d->flops_per_frame : 0.0; }
+
+int pa_preprocess_rgbd(const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws, int bgr, float near_m,
+                       float far_m, int H, int W, float* x_dev, void* stream) {
+  PA_CHECK(B >= 0, "batch");
+  if (B == 0) return PA_OK;
+  PA_CHECK(rgb_dev && depth_dev && x_dev, "null pointer");
+  return pa::launch_preprocess(rgb_dev, depth_dev, B, Hs, Ws, bgr, near_m, far_m, H, W, x_dev, (hipStream_t)stream);
+}
+
+int pa_keypoints_postprocess(const float* y_dev, const float* target_dev, int B, int n_kp, int H, int W,
+                             float* px_dev, float* loss_dev, void* stream) {
+  PA_CHECK(B >= 0 && n_kp > 0, "bad shape");
+  if (B == 0) return PA_OK;
+  PA_CHECK(y_dev && px_dev, "null pointer");
+  return pa::launch_postprocess(y_dev, target_dev, B, n_kp, H, W, px_dev, loss_dev, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,509 @@
+// Smoother factor residual + Jacobian kernels (f64), one lane per factor.
+//
+// Replaces the GTSAM CustomFactor callbacks of perseus/smoother/factors.py
+// (PoseDynamicsFactor :54-142, ConstantVelocityFactor :160-171,
+// KeypointProjectionFactor :216-275) and the GTSAM 4.2 geometry they call
+// (Pose3 Expmap/Logmap/ExpmapDerivative/LogmapDerivative/compose/between/
+// transformFrom/transformTo, Rot3 Logmap incl. the trace ~ -1 branch,
+// PinholeCamera<Cal3_S2>::project with its cheirality check).
+//
+// Layout (HBM): poses are 12 f64 (R row-major, t), vectors 3 f64, pixels 2 f64,
+// Jacobians column-major per factor.  A wave's 64 factors read 64 consecutive
+// records, so every fetched line is fully used; the work is FP64 VALU bound,
+// well below HBM.  Tangent order [omega; v], right perturbation.
+#include <cmath>
+
+#include "common.h"
+
+namespace pa {
+
+struct M3 {
+  double a[9];  // row-major
+  __device__ double& operator()(int r, int c) { return a[r * 3 + c]; }
+  __device__ double operator()(int r, int c) const { return a[r * 3 + c]; }
+};
+struct V3 {
+  double x, y, z;
+};
+
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ M3 zero3() {
+  M3 m;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m.a[i] = 0.0;
+  return m;
+}
+__device__ __forceinline__ M3 eye3() {
+  M3 m = zero3();
+  m.a[0] = m.a[4] = m.a[8] = 1.0;
+  return m;
+}
+__device__ __forceinline__ M3 skew(V3 w) {
+  M3 m = zero3();
+  m(0, 1) = -w.z;
+  m(0, 2) = w.y;
+  m(1, 0) = w.z;
+  m(1, 2) = -w.x;
+  m(2, 0) = -w.y;
+  m(2, 1) = w.x;
+  return m;
+}
+__device__ __forceinline__ M3 mul(const M3& A, const M3& B) {
+  M3 C;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) C(r, c) = A(r, 0) * B(0, c) + A(r, 1) * B(1, c) + A(r, 2) * B(2, c);
+  return C;
+}
+__device__ __forceinline__ M3 tr(const M3& A) {
+  M3 C;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) C(r, c) = A(c, r);
+  return C;
+}
+__device__ __forceinline__ M3 add(const M3& A, const M3& B, double sb = 1.0) {
+  M3 C;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) C.a[i] = A.a[i] + sb * B.a[i];
+  return C;
+}
+__device__ __forceinline__ M3 scale(const M3& A, double s) {
+  M3 C;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) C.a[i] = s * A.a[i];
+  return C;
+}
+__device__ __forceinline__ V3 mv(const M3& A, V3 v) {
+  return v3(A(0, 0) * v.x + A(0, 1) * v.y + A(0, 2) * v.z, A(1, 0) * v.x + A(1, 1) * v.y + A(1, 2) * v.z,
+            A(2, 0) * v.x + A(2, 1) * v.y + A(2, 2) * v.z);
+}
+__device__ __forceinline__ V3 mtv(const M3& A, V3 v) {  // A^T v
+  return v3(A(0, 0) * v.x + A(1, 0) * v.y + A(2, 0) * v.z, A(0, 1) * v.x + A(1, 1) * v.y + A(2, 1) * v.z,
+            A(0, 2) * v.x + A(1, 2) * v.y + A(2, 2) * v.z);
+}
+
+struct Pose {
+  M3 R;
+  V3 t;
+};
+
+__device__ __forceinline__ Pose load_pose(const double* p) {
+  Pose T;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) T.R.a[i] = p[i];
+  T.t = v3(p[9], p[10], p[11]);
+  return T;
+}
+__device__ __forceinline__ V3 load3(const double* p) { return v3(p[0], p[1], p[2]); }
+
+constexpr double kEps = 2.220446049250313e-16;  // std::numeric_limits<double>::epsilon()
+
+// Rot3::Expmap (so3::ExpmapFunctor)
+__device__ M3 rot_exp(V3 w) {
+  const double th2 = dot(w, w);
+  M3 W = skew(w);
+  if (th2 <= kEps) return add(eye3(), W);
+  const double th = sqrt(th2);
+  double s, c;
+  sincos(th, &s, &c);
+  return add(add(eye3(), W, s / th), mul(W, W), (1.0 - c) / th2);
+}
+
+// Rot3::Logmap (SO3::Logmap), incl. the trace ~ -1 branch
+__device__ V3 rot_log(const M3& R) {
+  const double R11 = R(0, 0), R12 = R(0, 1), R13 = R(0, 2);
+  const double R21 = R(1, 0), R22 = R(1, 1), R23 = R(1, 2);
+  const double R31 = R(2, 0), R32 = R(2, 1), R33 = R(2, 2);
+  const double trc = R11 + R22 + R33;
+  if (trc + 1.0 < 1e-3) {
+    double Wv, Q1, Q2, Q3;
+    V3 vec;
+    if (R33 > R22 && R33 > R11) {
+      Wv = R21 - R12;
+      Q1 = 2.0 + 2.0 * R33;
+      Q2 = R31 + R13;
+      Q3 = R23 + R32;
+      vec = v3(Q2, Q3, Q1);
+    } else if (R22 > R11) {
+      Wv = R13 - R31;
+      Q1 = 2.0 + 2.0 * R22;
+      Q2 = R23 + R32;
+      Q3 = R12 + R21;
+      vec = v3(Q3, Q1, Q2);
+    } else {
+      Wv = R32 - R23;
+      Q1 = 2.0 + 2.0 * R11;
+      Q2 = R12 + R21;
+      Q3 = R31 + R13;
+      vec = v3(Q1, Q2, Q3);
+    }
+    const double r = sqrt(Q1);
+    const double nrm = sqrt(Q1 * Q1 + Q2 * Q2 + Q3 * Q3 + Wv * Wv);
+    const double sgn = Wv < 0 ? -1.0 : 1.0;
+    const double mag = M_PI - (2.0 * sgn * Wv) / nrm;
+    const double sc = 0.5 / r * mag;
+    return (sgn * sc) * vec;
+  }
+  const double tr3 = trc - 3.0;
+  double mag;
+  if (tr3 < -1e-6) {
+    const double th = acos((trc - 1.0) / 2.0);
+    mag = th / (2.0 * sin(th));
+  } else {
+    mag = 0.5 - tr3 / 12.0 + tr3 * tr3 / 60.0;
+  }
+  return mag * v3(R32 - R23, R13 - R31, R21 - R12);
+}
+
+// SO3 ExpmapDerivative (right Jacobian) and LogmapDerivative (its inverse)
+__device__ M3 rot_dexp(V3 w) {
+  const double th2 = dot(w, w);
+  M3 W = skew(w);
+  if (th2 <= kEps) return add(eye3(), W, -0.5);
+  const double th = sqrt(th2);
+  double s, c;
+  sincos(th, &s, &c);
+  return add(add(eye3(), W, -(1.0 - c) / th2), mul(W, W), (th - s) / (th2 * th));
+}
+__device__ M3 rot_dlog(V3 w) {
+  const double th2 = dot(w, w);
+  if (th2 <= kEps) return eye3();
+  const double th = sqrt(th2);
+  double s, c;
+  sincos(th, &s, &c);
+  M3 W = skew(w);
+  return add(add(eye3(), W, 0.5), mul(W, W), 1.0 / th2 - (1.0 + c) / (2.0 * th * s));
+}
+
+// Pose3::Expmap
+__device__ Pose pose_exp(V3 w, V3 v) {
+  Pose T;
+  T.R = rot_exp(w);
+  const double th2 = dot(w, w);
+  if (th2 > kEps) {
+    V3 wxv = cross(w, v);
+    T.t = (1.0 / th2) * (wxv - mv(T.R, wxv) + dot(w, v) * w);
+  } else {
+    T.t = v;
+  }
+  return T;
+}
+
+// Pose3::Logmap (Agrawal06iros eq. 14)
+__device__ void pose_log(const Pose& T, V3& w, V3& u) {
+  w = rot_log(T.R);
+  const double th = sqrt(dot(w, w));
+  if (th < 1e-10) {
+    u = T.t;
+    return;
+  }
+  M3 W = skew((1.0 / th) * w);
+  const double tn = tan(0.5 * th);
+  V3 WT = mv(W, T.t);
+  u = T.t - (0.5 * th) * WT + (1.0 - th / (2.0 * tn)) * mv(W, WT);
+}
+
+// Pose3::ComputeQforExpmapDerivative (Barfoot14tro eq. 102, right Jacobian)
+__device__ M3 compute_q(V3 w, V3 v) {
+  M3 V = skew(v), W = skew(w);
+  M3 WV = mul(W, V), VW = mul(V, W);
+  M3 WVW = mul(WV, W);
+  M3 WWV = mul(W, WV), VWW = mul(VW, W);
+  M3 WVWW = mul(WVW, W), WWVW = mul(W, WVW);
+  const double phi = sqrt(dot(w, w));
+  M3 t1 = add(add(WV, VW), WVW, -1.0);
+  M3 t2 = add(add(WWV, VWW), WVW, -3.0);
+  M3 t3 = add(WVWW, WWVW);
+  double c1, c2, c3;
+  if (fabs(phi) > 1e-5) {
+    double s, c;
+    sincos(phi, &s, &c);
+    const double p2 = phi * phi, p3 = p2 * phi, p4 = p2 * p2, p5 = p4 * phi;
+    c1 = (phi - s) / p3;
+    c2 = (1.0 - p2 / 2.0 - c) / p4;
+    c3 = -0.5 * ((1.0 - p2 / 2.0 - c) / p4 - 3.0 * (phi - s - p3 / 6.0) / p5);
+  } else {
+    c1 = 1.0 / 6.0;
+    c2 = -1.0 / 24.0;
+    c3 = 1.0 / 120.0;
+  }
+  M3 Q = scale(V, -0.5);
+  Q = add(Q, t1, c1);
+  Q = add(Q, t2, c2);
+  Q = add(Q, t3, c3);
+  return Q;
+}
+
+// 6x6 helpers: block matrices [[A, 0],[C, A]] (dexp / dlog / adjoint form)
+struct M6 {
+  double a[36];  // row-major
+  __device__ double& operator()(int r, int c) { return a[r * 6 + c]; }
+  __device__ double operator()(int r, int c) const { return a[r * 6 + c]; }
+};
+__device__ __forceinline__ M6 blk(const M3& A, const M3& C) {
+  M6 m;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      m(r, c) = A(r, c);
+      m(r, c + 3) = 0.0;
+      m(r + 3, c) = C(r, c);
+      m(r + 3, c + 3) = A(r, c);
+    }
+  return m;
+}
+__device__ __forceinline__ M6 mul6(const M6& A, const M6& B) {
+  M6 C;
+  for (int r = 0; r < 6; ++r)
+    for (int c = 0; c < 6; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) s += A(r, k) * B(k, c);
+      C(r, c) = s;
+    }
+  return C;
+}
+// Pose3::AdjointMap = [[R, 0], [skew(t) R, R]]
+__device__ __forceinline__ M6 adjoint(const Pose& T) { return blk(T.R, mul(skew(T.t), T.R)); }
+__device__ __forceinline__ Pose inverse(const Pose& T) {
+  Pose I;
+  I.R = tr(T.R);
+  I.t = -1.0 * mtv(T.R, T.t);
+  return I;
+}
+__device__ __forceinline__ Pose compose(const Pose& A, const Pose& B) {
+  Pose C;
+  C.R = mul(A.R, B.R);
+  C.t = mv(A.R, B.t) + A.t;
+  return C;
+}
+
+// -------------------------------------------------------------------- kernels
+__device__ __forceinline__ void store_colmajor(double* J, const M6& m, int rows, int col0, int ncols,
+                                               const double* isig) {
+  for (int c = 0; c < ncols; ++c)
+#pragma unroll
+    for (int r = 0; r < 6; ++r) J[c * rows + r] = m(r, col0 + c) * (isig ? isig[r] : 1.0);
+}
+
+__global__ __launch_bounds__(64) void dyn_kernel(int n, const double* __restrict__ T1p, const double* __restrict__ wp,
+                                                 const double* __restrict__ vp, const double* __restrict__ T2p,
+                                                 double dt, int vel_frame, const double* __restrict__ isig,
+                                                 double* __restrict__ r_out, double* __restrict__ J0,
+                                                 double* __restrict__ J1, double* __restrict__ J2,
+                                                 double* __restrict__ J3, double* __restrict__ err) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const Pose T1 = load_pose(T1p + (size_t)i * 12);
+  const Pose T2 = load_pose(T2p + (size_t)i * 12);
+  const V3 w = load3(wp + (size_t)i * 3);
+  V3 v = load3(vp + (size_t)i * 3);
+  V3 vb = v;
+  if (vel_frame == PA_VEL_WORLD) vb = mtv(T1.R, v);  // transformTo / unrotate (factors.py:100,134)
+  const V3 xw = dt * w, xv = dt * vb;
+  const Pose inc = pose_exp(xw, xv);   // Expmap (:104 / :136)
+  const Pose pred = compose(T1, inc);  // compose (:105)
+  const Pose rel = compose(inverse(pred), T2);  // between (:108)
+  V3 ew, ev;
+  pose_log(rel, ew, ev);  // Logmap (:109)
+  double r[6] = {ew.x, ew.y, ew.z, ev.x, ev.y, ev.z};
+  double rs[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) rs[k] = r[k] * (isig ? isig[k] : 1.0);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) r_out[(size_t)i * 6 + k] = rs[k];
+  if (err) {
+    double e = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) e += rs[k] * rs[k];
+    err[i] = 0.5 * e;
+  }
+  if (!(J0 || J1 || J2 || J3)) return;
+  // dlog = LogmapDerivative(rel) (:112)
+  const M3 Jw = rot_dlog(ew);
+  const M3 Qr = compute_q(ew, ev);
+  const M6 dlog = blk(Jw, scale(mul(mul(Jw, Qr), Jw), -1.0));
+  // drel_dpred = -Ad(rel^-1); dpred_dx0 = Ad(inc^-1)
+  M6 A = mul6(dlog, adjoint(inverse(rel)));
+#pragma unroll
+  for (int k = 0; k < 36; ++k) A.a[k] = -A.a[k];  // dlog * drel_dpred
+  const M6 H0 = mul6(A, adjoint(inverse(inc)));
+  // derr_dtwist = dt * dlog * drel_dpred * I * ExpmapDerivative(xi) (:117)
+  const M3 Jx = rot_dexp(xw);
+  M6 dtw = mul6(A, blk(Jx, compute_q(xw, xv)));
+#pragma unroll
+  for (int k = 0; k < 36; ++k) dtw.a[k] *= dt;
+  M6 h0 = H0;
+  M6 h2;  // columns 0..2 used
+  if (vel_frame == PA_VEL_WORLD) {
+    // H0[:, :3] += dtw[:, 3:] @ skew(vb)  (:122);  H2 = dtw[:, 3:] @ R1^T (:125)
+    const M3 S = skew(vb);
+    for (int r6 = 0; r6 < 6; ++r6)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        double s = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          s += dtw(r6, 3 + k) * S(k, c);
+          s2 += dtw(r6, 3 + k) * T1.R(c, k);  // (R1^T)(k, c) = R1(c, k)
+        }
+        h0(r6, c) += s;
+        h2(r6, c) = s2;
+      }
+  } else {
+    for (int r6 = 0; r6 < 6; ++r6)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) h2(r6, c) = dtw(r6, 3 + c);  // (:128)
+  }
+  if (J0) store_colmajor(J0 + (size_t)i * 36, h0, 6, 0, 6, isig);
+  if (J1) store_colmajor(J1 + (size_t)i * 18, dtw, 6, 0, 3, isig);
+  if (J2) store_colmajor(J2 + (size_t)i * 18, h2, 6, 0, 3, isig);
+  if (J3) store_colmajor(J3 + (size_t)i * 36, dlog, 6, 0, 6, isig);  // dlog * I (:130)
+}
+
+__global__ __launch_bounds__(64) void cv_kernel(int n, const double* __restrict__ v1, const double* __restrict__ v2,
+                                                const double* __restrict__ isig, double* __restrict__ r,
+                                                double* __restrict__ J0, double* __restrict__ J1,
+                                                double* __restrict__ err) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  double e = 0.0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double s = isig ? isig[k] : 1.0;
+    const double rk = (v2[(size_t)i * 3 + k] - v1[(size_t)i * 3 + k]) * s;
+    r[(size_t)i * 3 + k] = rk;
+    e += rk * rk;
+  }
+  if (err) err[i] = 0.5 * e;
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      const double s = isig ? isig[rr] : 1.0;
+      if (J0) J0[(size_t)i * 9 + c * 3 + rr] = (rr == c ? -1.0 : 0.0) * s;
+      if (J1) J1[(size_t)i * 9 + c * 3 + rr] = (rr == c ? 1.0 : 0.0) * s;
+    }
+}
+
+__global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restrict__ Tb, const double* __restrict__ pbp,
+                                                  const double* __restrict__ zp, const double* __restrict__ Kp,
+                                                  int k_stride, const double* __restrict__ Tcp, int tc_stride,
+                                                  const double* __restrict__ isig, double* __restrict__ r_out,
+                                                  double* __restrict__ J, double* __restrict__ err,
+                                                  int32_t* __restrict__ status) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const Pose T = load_pose(Tb + (size_t)i * 12);
+  const V3 pb = load3(pbp + (size_t)i * 3);
+  const double* K = Kp + (size_t)i * k_stride;
+  const double fx = K[0], fy = K[1], sk = K[2], u0 = K[3], v0 = K[4];
+  Pose C;
+  if (Tcp) {
+    C = load_pose(Tcp + (size_t)i * tc_stride);
+  } else {
+    C.R = eye3();
+    C.t = v3(0, 0, 0);
+  }
+  // transformFrom (factors.py:257): pw = R pb + t, d/dpose = [R skew(-pb), R]
+  const V3 pw = mv(T.R, pb) + T.t;
+  // PinholeCamera::project (:260-261): pc = Rc^T (pw - tc), cheirality pc.z <= 0
+  const V3 pc = mtv(C.R, pw - C.t);
+  const double s0 = isig ? isig[0] : 1.0, s1 = isig ? isig[1] : 1.0;
+  if (!(pc.z > 0.0)) {
+    const double nan = __builtin_nan("");
+    r_out[(size_t)i * 2] = nan;
+    r_out[(size_t)i * 2 + 1] = nan;
+    if (J)
+      for (int k = 0; k < 12; ++k) J[(size_t)i * 12 + k] = nan;
+    if (err) err[i] = nan;
+    if (status) status[i] = 1;
+    return;
+  }
+  const double iz = 1.0 / pc.z;
+  const double x = pc.x * iz, y = pc.y * iz;
+  const double u = fx * x + sk * y + u0, v = fy * y + v0;
+  const double r0 = (u - zp[(size_t)i * 2]) * s0, r1 = (v - zp[(size_t)i * 2 + 1]) * s1;
+  r_out[(size_t)i * 2] = r0;
+  r_out[(size_t)i * 2 + 1] = r1;
+  if (err) err[i] = 0.5 * (r0 * r0 + r1 * r1);
+  if (status) status[i] = 0;
+  if (!J) return;
+  // dproj_dpoint = Dcal * Dpn * Rc^T (2x3), Dcal = [[fx, s],[0, fy]], Dpn = 1/z [[1,0,-x],[0,1,-y]]
+  double Dpn[2][3] = {{iz, 0.0, -x * iz}, {0.0, iz, -y * iz}};
+  double Dp[2][3];
+  for (int c = 0; c < 3; ++c) {
+    Dp[0][c] = fx * Dpn[0][c] + sk * Dpn[1][c];
+    Dp[1][c] = fy * Dpn[1][c];
+  }
+  double Dw[2][3];  // * Rc^T : (Rc^T)(k, c) = Rc(c, k)
+  for (int rr = 0; rr < 2; ++rr)
+    for (int c = 0; c < 3; ++c) Dw[rr][c] = Dp[rr][0] * C.R(c, 0) + Dp[rr][1] * C.R(c, 1) + Dp[rr][2] * C.R(c, 2);
+  // dpc_dpose = [R skew(-pb), R]
+  const M3 RS = mul(T.R, skew(-1.0 * pb));
+  double* Jo = J + (size_t)i * 12;
+  for (int c = 0; c < 6; ++c) {
+    double h[2];
+    for (int rr = 0; rr < 2; ++rr) {
+      double s = 0.0;
+      for (int k = 0; k < 3; ++k) s += Dw[rr][k] * (c < 3 ? RS(k, c) : T.R(k, c - 3));
+      h[rr] = s;
+    }
+    Jo[c * 2] = h[0] * s0;  // H0 = dproj_dpoint @ dpc_dpose (:264), column-major
+    Jo[c * 2 + 1] = h[1] * s1;
+  }
+}
+
+}  // namespace pa
+
+extern "C" {
+
+int pa_dyn_linearize(int n, const double* t1, const double* w, const double* v, const double* t2, double dt,
+                     int vel_frame, const double* inv_sigma, double* r, double* j0, double* j1, double* j2,
+                     double* j3, double* err, void* stream) {
+  PA_CHECK(n >= 0, "n %d", n);
+  if (n == 0) return PA_OK;
+  PA_CHECK(t1 && w && v && t2 && r, "null pointer");
+  PA_CHECK(vel_frame == PA_VEL_WORLD || vel_frame == PA_VEL_BODY, "vel_frame must be 'world' or 'body'.");
+  hipLaunchKernelGGL(pa::dyn_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, n, t1, w, v, t2, dt,
+                     vel_frame, inv_sigma, r, j0, j1, j2, j3, err);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+int pa_cv_linearize(int n, const double* v1, const double* v2, const double* inv_sigma, double* r, double* j0,
+                    double* j1, double* err, void* stream) {
+  PA_CHECK(n >= 0, "n %d", n);
+  if (n == 0) return PA_OK;
+  PA_CHECK(v1 && v2 && r, "null pointer");
+  hipLaunchKernelGGL(pa::cv_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, n, v1, v2, inv_sigma, r,
+                     j0, j1, err);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+int pa_proj_linearize(int n, const double* tbody, const double* pb, const double* z, const double* k, int k_stride,
+                      const double* tcam, int tcam_stride, const double* inv_sigma, double* r, double* j, double* err,
+                      int32_t* status, void* stream) {
+  PA_CHECK(n >= 0, "n %d", n);
+  if (n == 0) return PA_OK;
+  PA_CHECK(tbody && pb && z && k && r, "null pointer");
+  PA_CHECK(k_stride == 0 || k_stride == 5, "k_stride must be 0 or 5");
+  PA_CHECK(tcam_stride == 0 || tcam_stride == 12, "tcam_stride must be 0 or 12");
+  hipLaunchKernelGGL(pa::proj_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, n, tbody, pb, z, k,
+                     k_stride, tcam, tcam_stride, inv_sigma, r, j, err, status);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+}  // extern "C"

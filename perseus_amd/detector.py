@@ -1,0 +1,229 @@
+"""Drop-in `KeypointCNN` backed by the gfx950 HIP kernels of libperseus_amd.so.
+
+Mirrors `perseus/detector/models.py:6-40`:
+  * `KeypointCNN(n_keypoints=8, num_channels=3, H=256, W=256)` with attributes
+    `.n_keypoints .num_channels .H .W` (read by validate.py:176, streaming.py:130);
+  * `state_dict()` / `load_state_dict()` with torchvision resnet18 key names under
+    `resnet.` (122 keys incl. 20 `num_batches_tracked`), so checkpoints saved by the
+    reference's train.py (`torch.save(model.state_dict())`, train.py:351-355) load
+    unchanged after the callers' own `module.` stripping (validate.py:93-97);
+  * `forward(x)`: x (B, C, H, W) f32 -> (B, 2K) f32 normalized keypoints.
+
+Nothing here computes on the CPU: the parameters are plain containers (there is no
+torch conv graph behind them), and forward calls the C ABI.  A CPU input tensor (as in
+scripts/streaming.py:126-128, which never moves the model) is copied to the current
+GPU, run there, and the result copied back to the input's device.
+
+Differences from the reference (documented in DESIGN.md): inference only (no
+autograd, `train()` mode is not supported), only 256x256 inputs, num_channels 1-4.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from .synth import float_keys, resnet18_shapes
+
+
+class _Conv(nn.Module):
+    def __init__(self, shape):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(shape), requires_grad=False)
+
+
+class _BN(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(c), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(c), requires_grad=False)
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+
+class _Linear(nn.Module):
+    def __init__(self, out_f, in_f):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(out_f, in_f), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(out_f), requires_grad=False)
+
+
+class _Block(nn.Module):
+    def __init__(self, cin, cout, ds):
+        super().__init__()
+        self.conv1 = _Conv((cout, cin, 3, 3))
+        self.bn1 = _BN(cout)
+        self.conv2 = _Conv((cout, cout, 3, 3))
+        self.bn2 = _BN(cout)
+        if ds:
+            self.downsample = nn.ModuleDict({"0": _Conv((cout, cin, 1, 1)), "1": _BN(cout)})
+
+
+class _ResNet18Params(nn.Module):
+    """Parameter tree with torchvision.models.resnet18's names (no forward)."""
+
+    def __init__(self, in_ch, n_out):
+        super().__init__()
+        self.conv1 = _Conv((64, in_ch, 7, 7))
+        self.bn1 = _BN(64)
+        cin = 64
+        for li, cout in enumerate((64, 128, 256, 512), start=1):
+            ds = li > 1
+            self.add_module(f"layer{li}", nn.ModuleDict({"0": _Block(cin, cout, ds), "1": _Block(cout, cout, False)}))
+            cin = cout
+        self.fc = _Linear(n_out, 512)
+
+
+class KeypointCNN(nn.Module):
+    """Default perseus keypoint CNN (ResNet-18 regressor), HIP/MFMA implementation."""
+
+    def __init__(self, n_keypoints: int = 8, num_channels: int = 3, H: int = 256, W: int = 256,
+                 precision: str = "fp16") -> None:
+        super().__init__()
+        if (H, W) != (256, 256):
+            raise ValueError(f"only 256x256 inputs are supported, got {H}x{W}")
+        if not 1 <= num_channels <= 4:
+            raise ValueError(f"num_channels must be in [1, 4], got {num_channels}")
+        self.resnet = _ResNet18Params(num_channels, 2 * n_keypoints)
+        self.n_keypoints = n_keypoints
+        self.num_channels = num_channels
+        self.H = H
+        self.W = W
+        self.precision = precision
+        self._handle = None
+        self._handle_dev = None
+        self._stamp = None
+        self.eval()
+
+    # -------------------------------------------------------------- weights
+    def _fingerprint(self):
+        return tuple((t._version, t.data_ptr()) for t in self.state_dict(keep_vars=True).values())
+
+    def _blob(self) -> np.ndarray:
+        sd = self.state_dict()
+        shapes = resnet18_shapes(self.num_channels, self.n_keypoints)
+        parts = [sd[k].detach().to("cpu", torch.float32).reshape(-1).numpy() for k in float_keys(shapes)]
+        return np.ascontiguousarray(np.concatenate(parts))
+
+    def _ensure_handle(self, device: torch.device):
+        stamp = self._fingerprint()
+        if self._handle is not None and self._stamp == stamp and self._handle_dev == device:
+            return self._handle
+        self._release()
+        L = _lib.lib()
+        blob = self._blob()
+        h = _lib.C.c_void_p()
+        with torch.cuda.device(device):
+            _lib.check(L.pa_detector_create(blob.ctypes.data, blob.nbytes, self.num_channels, self.n_keypoints,
+                                            self.H, self.W, _lib.C.byref(h)), "pa_detector_create")
+        self._handle = h
+        self._handle_dev = device
+        self._stamp = stamp
+        return h
+
+    def _release(self):
+        if self._handle is not None:
+            _lib.lib().pa_detector_destroy(self._handle)
+            self._handle = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    def train(self, mode: bool = True):
+        if mode:
+            raise NotImplementedError("perseus_amd.KeypointCNN is inference-only (train.py is out of scope)")
+        return super().train(False)
+
+    def reserve(self, max_batch: int, device=None):
+        device = torch.device(device or torch.device("cuda", torch.cuda.current_device()))
+        h = self._ensure_handle(device)
+        _lib.check(_lib.lib().pa_detector_reserve(h, max_batch), "reserve")
+
+    def flops_per_frame(self) -> float:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        return _lib.lib().pa_detector_flops_per_frame(self._ensure_handle(dev))
+
+    # -------------------------------------------------------------- forward
+    def _prep(self, x: torch.Tensor):
+        if x.dim() != 4 or x.shape[1] != self.num_channels or x.shape[2] != self.H or x.shape[3] != self.W:
+            raise RuntimeError(f"expected input of shape (B, {self.num_channels}, {self.H}, {self.W}), "
+                               f"got {tuple(x.shape)}")
+        out_dev = x.device
+        if x.device.type != "cuda":
+            if not torch.cuda.is_available():
+                raise RuntimeError("perseus_amd.KeypointCNN needs a ROCm GPU (no CPU fallback)")
+            x = x.to(torch.device("cuda", torch.cuda.current_device()), non_blocking=False)
+        x = x.to(torch.float32).contiguous()
+        return x, out_dev
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x, out_dev = self._prep(x)
+        dev = x.device
+        h = self._ensure_handle(dev)
+        L = _lib.lib()
+        _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP32 if self.precision == "fp32" else _lib.PREC_FP16),
+                   "set_precision")
+        y = torch.empty((x.shape[0], 2 * self.n_keypoints), dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            _lib.check(L.pa_detector_forward(h, x.data_ptr(), x.shape[0], y.data_ptr(), _lib.stream_of(dev)),
+                       "pa_detector_forward")
+        return y if out_dev == dev else y.to(out_dev)
+
+    def profile(self, x: torch.Tensor, max_kernels: int = 64):
+        """Per-kernel device times (ms) of one forward, via HIP events in the library."""
+        x, _ = self._prep(x)
+        dev = x.device
+        h = self._ensure_handle(dev)
+        L = _lib.lib()
+        _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP32 if self.precision == "fp32" else _lib.PREC_FP16),
+                   "set_precision")
+        y = torch.empty((x.shape[0], 2 * self.n_keypoints), dtype=torch.float32, device=dev)
+        ms = (_lib.C.c_float * max_kernels)()
+        names = (_lib.C.c_char_p * max_kernels)()
+        with torch.cuda.device(dev):
+            n = _lib.check(L.pa_detector_profile(h, x.data_ptr(), x.shape[0], y.data_ptr(), _lib.stream_of(dev),
+                                                 ms, names, max_kernels), "pa_detector_profile")
+        return [(names[i].decode(), ms[i]) for i in range(n)], y
+
+
+def denormalize_pixel_coordinates(y: torch.Tensor, H: int = 256, W: int = 256, target: torch.Tensor | None = None):
+    """Device post-processing (validate.py:130-153): normalized (B,2K) -> px (B,K,2),
+    plus SmoothL1(beta=1, reduction='none') against normalized targets if given."""
+    if y.device.type != "cuda":
+        raise RuntimeError("denormalize_pixel_coordinates expects a device tensor")
+    y = y.contiguous().float()
+    B, n2 = y.shape
+    px = torch.empty((B, n2 // 2, 2), dtype=torch.float32, device=y.device)
+    loss = None
+    tptr = None
+    if target is not None:
+        target = target.reshape(B, n2).contiguous().float()
+        loss = torch.empty_like(y)
+        tptr = target.data_ptr()
+    _lib.check(_lib.lib().pa_keypoints_postprocess(y.data_ptr(), tptr, B, n2 // 2, H, W, px.data_ptr(),
+                                                   None if loss is None else loss.data_ptr(),
+                                                   _lib.stream_of(y.device)), "postprocess")
+    return px if loss is None else (px, loss)
+
+
+def preprocess_rgbd(rgb: torch.Tensor, depth: torch.Tensor, H: int = 256, W: int = 256, bgr: bool = True,
+                    near: float | None = None, far: float | None = None) -> torch.Tensor:
+    """Device version of ZEDCamera.get_frame's arithmetic (streaming.py:59-82) +
+    deterministic near/far clip: uint8 (B,Hs,Ws,3) + f32 metres (B,Hs,Ws) ->
+    (B,4,H,W) f32 model input."""
+    if rgb.device.type != "cuda" or depth.device.type != "cuda":
+        raise RuntimeError("preprocess_rgbd expects device tensors")
+    rgb = rgb.contiguous()
+    depth = depth.contiguous().float()
+    B, Hs, Ws, _ = rgb.shape
+    x = torch.empty((B, 4, H, W), dtype=torch.float32, device=rgb.device)
+    _lib.check(_lib.lib().pa_preprocess_rgbd(rgb.data_ptr(), depth.data_ptr(), B, Hs, Ws, int(bgr),
+                                             -1.0 if near is None else near, -1.0 if far is None else far,
+                                             H, W, x.data_ptr(), _lib.stream_of(rgb.device)), "preprocess")
+    return x
