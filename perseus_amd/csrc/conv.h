@@ -20,6 +20,9 @@ template <typename T>
 int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);
 
 template <typename T>
+int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname);
+
+template <typename T>
 int launch_stem(const float* x, int B, int Cin, const T* w, const float* bias, T* out, hipStream_t s);
 
 template <typename T>

@@ -1,0 +1,361 @@
+// 3x3 stride-1 convolution with an LDS halo patch (the BasicBlock convs of
+// torchvision resnet18 after the first block of each stage; 13 of the 20 convs).
+//
+// Per workgroup: an output tile of NI images x TH x TW pixels x BN channels.
+// For every 128-byte channel block cb of the input, the (TH+2) x (TW+2) input
+// patch of each image is staged in LDS ONCE and read by all 9 filter taps
+// (implicit GEMM re-fetches every input pixel 9x); weights stream per
+// (cb, tap) through a 2-deep LDS ring.  Register-staged prefetch: the next
+// step's weight tile and, during a whole channel block, the next block's
+// patch are in flight while the MFMAs run.  One barrier per step.
+//
+// MFMA operand roles: A = weights (rows = output channels), B = pixels, so a
+// lane's 4 accumulators are 4 consecutive channels of ONE pixel and the
+// epilogue stores / residual loads straight from registers (8 B per lane for
+// fp16, 16 B for f32), no LDS staging.
+#include <type_traits>
+
+#include "conv.h"
+
+namespace pa {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T>
+struct PElem;
+template <>
+struct PElem<_Float16> {
+  static constexpr int KB = 64;
+};
+template <>
+struct PElem<float> {
+  static constexpr int KB = 32;
+};
+
+__device__ __forceinline__ int pswz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+template <typename T>
+__device__ __forceinline__ void pmma(f32x4& acc, const u32x4& a, const u32x4& b);
+
+template <>
+__device__ __forceinline__ void pmma<_Float16>(f32x4& acc, const u32x4& a, const u32x4& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), acc, 0, 0,
+                                               0);
+}
+template <>
+__device__ __forceinline__ void pmma<float>(f32x4& acc, const u32x4& a, const u32x4& b) {
+  f32x4 fa = __builtin_bit_cast(f32x4, a), fb = __builtin_bit_cast(f32x4, b);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[0], fb[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[1], fb[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[2], fb[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[3], fb[3], acc, 0, 0, 0);
+}
+
+// 4 consecutive elements <-> f32
+__device__ __forceinline__ void ld4(const _Float16* p, float* v) {
+  half4 h = *reinterpret_cast<const half4*>(p);
+  v[0] = (float)h[0];
+  v[1] = (float)h[1];
+  v[2] = (float)h[2];
+  v[3] = (float)h[3];
+}
+__device__ __forceinline__ void ld4(const float* p, float* v) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  v[0] = a[0];
+  v[1] = a[1];
+  v[2] = a[2];
+  v[3] = a[3];
+}
+__device__ __forceinline__ void st4(_Float16* p, const float* v) {
+  half4 h;
+  h[0] = (_Float16)v[0];
+  h[1] = (_Float16)v[1];
+  h[2] = (_Float16)v[2];
+  h[3] = (_Float16)v[3];
+  *reinterpret_cast<half4*>(p) = h;
+}
+__device__ __forceinline__ void st4(float* p, const float* v) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+}
+
+// Lane -> pixel map of a 16-pixel MFMA fragment: lanes whose ds_read_b128 lane
+// groups read chunk c0 take the even pixel offsets, the others the odd ones, so
+// with the (p >> 1) & 7 XOR swizzle every 16-lane group hits 16 distinct bank
+// slots for ANY starting pixel (the 9 taps shift the start by 1 and by PW).
+__device__ __forceinline__ int frag_off(int r) { return r < 4 ? 2 * r : (r < 12 ? 2 * (r - 4) + 1 : 2 * (r - 8)); }
+
+template <int V>
+using ic = std::integral_constant<int, V>;
+
+template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int EPI>
+__global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int KB = PElem<T>::KB;
+  constexpr int CPR = 16 / sizeof(T);
+  constexpr int NCB = CIN / KB;  // 128-byte channel blocks
+  constexpr int NSTEPS = NCB * 9;
+  constexpr int KTOT = 9 * CIN;
+  constexpr int PH = TH + 2, PW = TW + 2;
+  // per-image patch stride in pixels; for 8-wide tiles a fragment pairs one row of
+  // two images, which is conflict-free when the image stride is 8 mod 16
+  constexpr int IMS = (TW == 8) ? ((PH * PW + 7) / 16 * 16 + 8) : PH * PW;
+  constexpr int NP = NI * IMS;  // patch pixels (incl. pad)
+  constexpr int BM = NI * TH * TW;
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int PCH = (NP * 8 + NT - 1) / NT;  // patch 16-B chunks per thread
+  constexpr int BCH = BN * 8 / NT;             // weight chunks per thread
+  static_assert(BN * 8 % NT == 0, "weight tile / threads");
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+  static_assert(TW >= 16 || (TW == 8 && NI == 2), "fragment geometry");
+  static_assert(PBUF == 2 || NCB == 1 || true, "");
+  constexpr int PATCHB = NP * 128;
+  constexpr int WB = BN * 128;
+  __shared__ __attribute__((aligned(16))) char smem[PBUF * PATCHB + 2 * WB];
+  char* patch = smem;
+  char* wbuf = smem + PBUF * PATCHB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int H = a.Hout, W = a.Wout;
+  constexpr int Cin = CIN;
+  const int Cout = a.Cout;
+  const T* __restrict__ in = (const T*)a.in;
+  const T* __restrict__ w = (const T*)a.w;
+
+  // tile decode: N-tiles of one spatial tile are adjacent (share the patch in L2)
+  const int ntn = Cout / BN;
+  const int tn_idx = blockIdx.x % ntn;
+  const int sp = blockIdx.x / ntn;
+  const int tw_n = W / TW, tpi = (H / TH) * tw_n;
+  const int img0 = (sp / tpi) * NI;
+  const int rem = sp - (sp / tpi) * tpi;
+  const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
+  const int n0 = tn_idx * BN;
+
+  // ---- staging (register-staged; hipcc counts these loads itself)
+  u32x4 rp[PCH];
+  u32x4 rb[3][BCH];
+  auto load_patch = [&](int cb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PCH; ++i) {
+      const int c = tid + i * NT;
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (c < NP * 8) {
+        const int p = c >> 3, ch = c & 7;
+        const int img = p / IMS, pp = p - (p / IMS) * IMS;
+        const int pr = pp / PW, pc = pp - (pp / PW) * PW;
+        const int n = img0 + img, h = th0 + pr - 1, x = tw0 + pc - 1;
+        if (pr < PH && n < a.B && (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W)
+          v = *reinterpret_cast<const u32x4*>(in + (((size_t)n * H + h) * W + x) * Cin + cb * KB + ch * CPR);
+      }
+      rp[i] = v;
+    }
+  };
+  auto store_patch = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PCH; ++i) {
+      const int c = tid + i * NT;
+      if (c < NP * 8) *reinterpret_cast<u32x4*>(patch + buf * PATCHB + pswz(c >> 3, c & 7)) = rp[i];
+    }
+  };
+  auto load_w = [&](int s, auto setc) __attribute__((always_inline)) {
+    constexpr int SET = decltype(setc)::value;
+    const int cb = s / 9, tap = s - (s / 9) * 9;
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * NT;
+      const int row = c >> 3, ch = c & 7;
+      rb[SET][i] = *reinterpret_cast<const u32x4*>(w + (size_t)(n0 + row) * KTOT + tap * Cin + cb * KB + ch * CPR);
+    }
+  };
+  auto store_w = [&](int buf, auto setc) __attribute__((always_inline)) {
+    constexpr int SET = decltype(setc)::value;
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int c = tid + i * NT;
+      *reinterpret_cast<u32x4*>(wbuf + buf * WB + pswz(c >> 3, c & 7)) = rb[SET][i];
+    }
+  };
+
+  // per-lane patch pixel (tap (0,0)) of each pixel fragment
+  const int o = frag_off(r16);
+  int ppix[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int mb = wm * WTM + tm * 16;  // first m of the fragment
+    if constexpr (TW == 8) {
+      const int y = mb / 16;  // m = (y * 2 + img) * 8 + x
+      ppix[tm] = (o >> 3) * IMS + y * PW + (o & 7);
+    } else {
+      const int img = mb / (TH * TW);
+      const int y = (mb / TW) % TH, x = mb % TW + o;
+      ppix[tm] = img * IMS + y * PW + x;
+    }
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_patch(0);
+  load_w(0, ic<0>{});
+  store_patch(0);
+  store_w(0, ic<0>{});
+  load_w(NSTEPS > 1 ? 1 : 0, ic<1>{});
+  load_w(NSTEPS > 2 ? 2 : 0, ic<2>{});
+  __syncthreads();
+
+  // One K-step (cb, TAP): refill register set TAP%3 with W(s+3), MFMAs on the
+  // staged W(s) and patch(cb), then W(s+1) (set (TAP+1)%3) -> the other LDS
+  // buffer.  Weight loads stay in flight for ~2 steps; the next block's patch
+  // for the whole channel block.  Every load/store is unconditional (indices are
+  // clamped) so that hipcc's vmcnt bookkeeping stays exact.
+  auto step = [&](int cb, auto tapc) __attribute__((always_inline)) {
+    constexpr int TAP = decltype(tapc)::value;
+    constexpr int KR = TAP / 3, KC = TAP % 3;
+    const int s = cb * 9 + TAP;
+    load_w(s + 3 < NSTEPS ? s + 3 : NSTEPS - 1, ic<TAP % 3>{});
+    if constexpr (TAP == 0 && NCB > 1) load_patch(cb + 1 < NCB ? cb + 1 : NCB - 1);
+    const char* pb = patch + (PBUF == 2 ? (cb & 1) * PATCHB : 0);
+    const char* wb = wbuf + (s & 1) * WB;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      u32x4 fa[TN], fb[TM];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        fa[tn] = *reinterpret_cast<const u32x4*>(wb + pswz(wn * WTN + tn * 16 + r16, g * 4 + q));
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+        fb[tm] = *reinterpret_cast<const u32x4*>(pb + pswz(ppix[tm] + KR * PW + KC, g * 4 + q));
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) pmma<T>(acc[tm][tn], fa[tn], fb[tm]);
+    }
+    store_w((s + 1) & 1, ic<(TAP + 1) % 3>{});
+    if constexpr (NCB > 1 && TAP == 8) {
+      if constexpr (PBUF == 2) {
+        store_patch((cb + 1) & 1);
+        __syncthreads();
+      } else {
+        __syncthreads();  // single patch buffer: overwrite after every wave is done with it
+        store_patch(0);
+        __syncthreads();
+      }
+    } else {
+      __syncthreads();
+    }
+  };
+  for (int cb = 0; cb < NCB; ++cb) {
+    step(cb, ic<0>{});
+    step(cb, ic<1>{});
+    step(cb, ic<2>{});
+    step(cb, ic<3>{});
+    step(cb, ic<4>{});
+    step(cb, ic<5>{});
+    step(cb, ic<6>{});
+    step(cb, ic<7>{});
+    step(cb, ic<8>{});
+  }
+
+  // ---- epilogue straight from registers: lane holds channels co..co+3 of one pixel.
+  // All residual/bias loads are issued before any use (no serial load->use chains).
+  const T* __restrict__ res = (const T*)a.res;
+  T* __restrict__ out = (T*)a.out;
+  size_t pixo[TM];
+  bool ok[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int mb = wm * WTM + tm * 16;
+    int img, y, x;
+    if constexpr (TW == 8) {
+      y = mb / 16;
+      img = o >> 3;
+      x = o & 7;
+    } else {
+      img = mb / (TH * TW);
+      y = (mb / TW) % TH;
+      x = mb % TW + o;
+    }
+    const int n = img0 + img;
+    ok[tm] = n < a.B;
+    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * Cout;
+  }
+  f32x4 bias[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + n0 + wn * WTN + tn * 16 + q * 4);
+  float rv[TM][TN][4];
+  if constexpr (EPI & EPI_RES) {
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) ld4(res + pixo[tm] + n0 + wn * WTN + tn * 16 + q * 4, rv[tm][tn]);
+  }
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    if (!ok[tm]) continue;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = acc[tm][tn][j] + bias[tn][j];
+        if constexpr (EPI & EPI_RES) v[j] += rv[tm][tn][j];
+        if constexpr (EPI & EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+      }
+      st4(out + pixo[tm] + n0 + wn * WTN + tn * 16 + q * 4, v);
+    }
+  }
+}
+
+template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN>
+static int run_patch(const ConvArgs& a, hipStream_t s) {
+  PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "patch conv: epilogue %d", a.epi);
+  PA_CHECK(a.Cin == CIN, "patch conv: Cin %d != %d", a.Cin, CIN);
+  PA_CHECK(a.Hout % TH == 0 && a.Wout % TW == 0, "patch conv: %dx%d not tiled by %dx%d", a.Hout, a.Wout, TH, TW);
+  PA_CHECK(a.Cout % BN == 0, "patch conv: Cout %d %% BN %d", a.Cout, BN);
+  const int tiles = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW) * (a.Cout / BN);
+  if (a.epi & EPI_RES)
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES>), dim3(tiles),
+                       dim3(WM * WN * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU>), dim3(tiles),
+                       dim3(WM * WN * 64), 0, s, a);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+// Stride-1 3x3 conv, Hin == Hout.  Tile configuration per feature-map size.
+template <typename T>
+int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
+  PA_CHECK(a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout, "patch conv: stride-1 only");
+  PA_CHECK(a.Cin % PElem<T>::KB == 0, "patch conv: Cin %d", a.Cin);
+  if (a.B <= 0) return PA_OK;
+  if (a.Hout == 64 && a.Cout == 64) {
+    if (kname) *kname = "conv3x3p_l1";
+    return run_patch<T, 16, 32, 1, 64, 8, 1, 1, 64>(a, s);
+  }
+  if (a.Hout == 32) {
+    if (kname) *kname = "conv3x3p_l2";
+    return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128>(a, s);
+  }
+  if (a.Hout == 16) {
+    if (kname) *kname = "conv3x3p_l3";
+    return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256>(a, s);
+  }
+  if (a.Hout == 8) {
+    if (kname) *kname = "conv3x3p_l4";
+    return run_patch<T, 8, 8, 2, 64, 2, 2, 2, 512>(a, s);
+  }
+  set_error("patch conv: no configuration for %dx%d", a.Hout, a.Wout);
+  return PA_EINVAL;
+}
+
+template int launch_conv3x3_s1<_Float16>(const ConvArgs&, hipStream_t, const char**);
+template int launch_conv3x3_s1<float>(const ConvArgs&, hipStream_t, const char**);
+
+}  // namespace pa

@@ -236,7 +236,10 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     a.stride = c1.stride;
     a.pad = 1;
     a.epi = EPI_RELU;
-    PA_TRY(launch_conv<T>(a, 3, s, &kn));
+    if (c1.stride == 1)
+      PA_TRY(launch_conv3x3_s1<T>(a, s, &kn));
+    else
+      PA_TRY(launch_conv<T>(a, 3, s, &kn));
     if (prof) prof->mark(kn);
     const T* res = X;
     T* out = X;  // identity block: residual add in place (same element, same thread)
@@ -271,7 +274,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     b2.stride = 1;
     b2.pad = 1;
     b2.epi = EPI_RELU | EPI_RES;
-    PA_TRY(launch_conv<T>(b2, 3, s, &kn));
+    PA_TRY(launch_conv3x3_s1<T>(b2, s, &kn));
     if (prof) prof->mark(kn);
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
