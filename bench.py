@@ -142,9 +142,10 @@ def main():
     return line
 
 
-def conv_flops(B):
+def conv_flops(B, fused_stem=True):
     """Algorithmic FLOPs per launch, in forward order (matches pa_detector_profile)."""
-    fl = [2.0 * B * 128 * 128 * 64 * 49 * 4, 0.0]  # stem (true K = 196), maxpool
+    stem = 2.0 * B * 128 * 128 * 64 * 49 * 4  # true K = 196
+    fl = [stem] if fused_stem else [stem, 0.0]  # fp16 fuses conv7x7 + maxpool
     hw, cin = 64, 64
     for li, cout in enumerate((64, 128, 256, 512)):
         for bi in range(2):
@@ -162,7 +163,7 @@ def conv_flops(B):
 
 
 def roofline(per_launch, B, precision):
-    fl = conv_flops(B)
+    fl = conv_flops(B, fused_stem=len(per_launch) == 21)
     if len(fl) != len(per_launch):
         return None
     groups = {}

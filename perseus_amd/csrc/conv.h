@@ -25,6 +25,9 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname);
 template <typename T>
 int launch_stem(const float* x, int B, int Cin, const T* w, const float* bias, T* out, hipStream_t s);
 
+int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,
+                          hipStream_t s);
+
 template <typename T>
 int launch_maxpool(const T* in, int B, int H, int W, int C, T* out, hipStream_t s);
 

@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "conv.h"
@@ -208,10 +209,16 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   T* D = Tb + act_el;
   if (prof) prof->mark("start");
   const ConvL& st = d->convs[0];
-  PA_TRY(launch_stem<T>(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, S, s));
-  if (prof) prof->mark("stem_conv7x7");
-  PA_TRY(launch_maxpool<T>(S, B, 128, 128, 64, X, s));
-  if (prof) prof->mark("maxpool");
+  if constexpr (std::is_same<T, _Float16>::value) {
+    // fused conv7x7 + BN + ReLU + maxpool: the 128x128 map stays on chip
+    PA_TRY(launch_stem_pool_fp16(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, X, s));
+    if (prof) prof->mark("stem_conv7x7_pool");
+  } else {
+    PA_TRY(launch_stem<T>(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, S, s));
+    if (prof) prof->mark("stem_conv7x7");
+    PA_TRY(launch_maxpool<T>(S, B, 128, 128, 64, X, s));
+    if (prof) prof->mark("maxpool");
+  }
   int hw = 64;
   for (const Block& b : d->blocks) {
     const ConvL& c1 = d->convs[b.conv1];

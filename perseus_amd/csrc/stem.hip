@@ -1,0 +1,207 @@
+// Fused RGBD stem for the fp16 path: conv 7x7 s2 p3 (Cin <= 4 -> 64) + folded BN
+// + ReLU + max-pool 3x3 s2 p1, reading the caller's f32 NCHW frames directly and
+// writing only the pooled fp16 NHWC map (torchvision resnet18 stem behind
+// perseus/detector/models.py:27-28,34-40).  The 128x128x64 conv map never
+// touches HBM.
+//
+// Workgroup = one image x PB pooled rows (all 64 columns, 64 channels).  Conv
+// rows are produced in pairs from a 16-row ring of input rows in LDS (f32->fp16
+// converted on the way in, 4 channels interleaved per pixel); each pair needs 9
+// input rows and brings in 4 new ones, prefetched into registers while the
+// MFMAs of the current pair run.  Conv rows (post-ReLU) go to a 3-row LDS ring;
+// pooled row p needs conv rows 2p-1, 2p, 2p+1, i.e. the previous pair's second
+// row and the current pair.  The band recomputes one halo conv row.
+//
+// GEMM per pair: M = 256 pixels, N = 64 channels, K = 7 kh x 32 (28 real: 7 kw
+// x 4 ch, 4 zero-weight pad) with MFMA A = weights, B = input patch.
+#include <type_traits>
+
+#include "conv.h"
+
+namespace pa {
+
+typedef unsigned su32x4 __attribute__((ext_vector_type(4)));
+
+namespace stem {
+constexpr int PB = 8;         // pooled rows per workgroup
+constexpr int NT = 512;       // 8 waves
+constexpr int RING = 16;      // input-row ring
+constexpr int PW = 262;       // ring row width in pixels (wi = c - 3)
+constexpr int ROWB = PW * 8;  // bytes per ring row (4 x fp16 per pixel)
+constexpr int WBYTES = 7 * 64 * 64;       // weights [kh][co][32 halves]
+constexpr int CROWB = 128 * 128;          // one conv row: 128 px x 64 ch fp16
+constexpr int LDS = RING * ROWB + WBYTES + 3 * CROWB;
+constexpr int F[4] = {0, 2, 3, 1};        // 64-B-row chunk swizzle (conflict-free A reads)
+}  // namespace stem
+
+__device__ __forceinline__ int stem_wswz(int kh, int co, int chunk) {
+  constexpr int F[4] = {0, 2, 3, 1};
+  return (kh * 64 + co) * 64 + ((chunk ^ F[(co >> 2) & 3]) << 4);
+}
+__device__ __forceinline__ int crow_swz(int px, int chunk) { return px * 128 + ((chunk ^ ((px >> 1) & 7)) << 4); }
+
+__global__ __launch_bounds__(512) void stem_pool_fp16(const float* __restrict__ x, int B, int Cin,
+                                                      const _Float16* __restrict__ w, const float* __restrict__ bias,
+                                                      _Float16* __restrict__ out) {
+  using namespace stem;
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  char* ring = smem;
+  char* wl = smem + RING * ROWB;
+  char* crow = wl + WBYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int n = blockIdx.y;
+  const int p0 = blockIdx.x * PB;
+  const float* xn = x + (size_t)n * Cin * 256 * 256;
+
+  // ---- weights [64][7][32] fp16 (global) -> LDS [kh][co][4 swizzled chunks]
+  for (int i = tid; i < 64 * 7 * 4; i += NT) {
+    const int co = i / 28, r = i - (i / 28) * 28, kh = r >> 2, ch = r & 3;
+    *reinterpret_cast<su32x4*>(wl + stem_wswz(kh, co, ch)) =
+        *reinterpret_cast<const su32x4*>(w + (size_t)co * 224 + kh * 32 + ch * 8);
+  }
+
+  // ---- input rows: thread t < 256 owns (row t/64 of the 4 new rows, 4 columns)
+  auto load_rows = [&](int hi0, float4* v) __attribute__((always_inline)) {
+    const int r = tid >> 6, cg = tid & 63;
+    const int hi = hi0 + r;
+    const bool ok = (unsigned)hi < 256u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      v[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok && c < Cin) v[c] = *reinterpret_cast<const float4*>(xn + ((size_t)c * 256 + hi) * 256 + cg * 4);
+    }
+  };
+  auto store_rows = [&](int hi0, const float4* v) __attribute__((always_inline)) {
+    const int r = tid >> 6, cg = tid & 63;
+    const int slot = (hi0 + r + 64) & (RING - 1);
+    char* row = ring + slot * ROWB;
+    // 4 pixels x 4 channels -> 32 contiguous bytes at pixel (cg*4 + 3)
+    _Float16 h[16];
+    h[0] = (_Float16)v[0].x; h[1] = (_Float16)v[1].x; h[2] = (_Float16)v[2].x; h[3] = (_Float16)v[3].x;
+    h[4] = (_Float16)v[0].y; h[5] = (_Float16)v[1].y; h[6] = (_Float16)v[2].y; h[7] = (_Float16)v[3].y;
+    h[8] = (_Float16)v[0].z; h[9] = (_Float16)v[1].z; h[10] = (_Float16)v[2].z; h[11] = (_Float16)v[3].z;
+    h[12] = (_Float16)v[0].w; h[13] = (_Float16)v[1].w; h[14] = (_Float16)v[2].w; h[15] = (_Float16)v[3].w;
+    // pixel cg*4+3 starts at byte (cg*4+3)*8: only 8-B aligned -> 4 x 8-B stores
+    uint2* d = reinterpret_cast<uint2*>(row + (cg * 4 + 3) * 8);
+    const uint2* s = reinterpret_cast<const uint2*>(h);
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+    d[3] = s[3];
+  };
+  // zero the 3 left / 3 right pad pixels of every ring row once (never rewritten)
+  for (int i = tid; i < RING * 6; i += NT) {
+    const int slot = i / 6, k = i - (i / 6) * 6;
+    const int px = k < 3 ? k : 256 + k;  // 0,1,2 and 259,260,261
+    *reinterpret_cast<uint2*>(ring + slot * ROWB + px * 8) = make_uint2(0, 0);
+  }
+  // prologue: the 9 input rows of pair 0 (hi = 4*p0 - 7 .. 4*p0 + 1)
+  const int hbase = 4 * p0 - 7;
+  {
+    float4 v[4];
+    for (int k = 0; k < 9; k += 4) {
+      if (tid < 256 && (tid >> 6) + k < 9) {
+        load_rows(hbase + k, v);
+        store_rows(hbase + k, v);
+      }
+    }
+  }
+  __syncthreads();
+
+  // wave w: pixels [32w, 32w+32) of the pair (conv row w>>2, cols (w&3)*32..), all 64 channels
+  constexpr int TM = 2, TN = 4;
+  const int hr = wid >> 2, wo0 = (wid & 3) * 32;
+  float4 nv[4];
+  f32x4 bv[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) bv[tn] = *reinterpret_cast<const f32x4*>(bias + tn * 16 + q * 4);
+
+  for (int j = 0; j <= PB; ++j) {
+    const int r0 = 2 * p0 - 2 + 2 * j;  // conv rows r0, r0+1
+    const int hs = 4 * p0 - 7 + 4 * j;  // first input row of this pair
+    if (j < PB && tid < 256) load_rows(hs + 9, nv);
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      const int slot = (hs + 2 * hr + kh + 64) & (RING - 1);
+      const char* row = ring + slot * ROWB;
+      su32x4 fa[TN], fb[TM];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        fa[tn] = *reinterpret_cast<const su32x4*>(wl + stem_wswz(kh, tn * 16 + r16, q));
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int wo = wo0 + tm * 16 + r16;
+        fb[tm] = *reinterpret_cast<const su32x4*>(row + (2 * wo) * 8 + q * 16);
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[tn]),
+                                                               __builtin_bit_cast(half8, fb[tm]), acc[tm][tn], 0, 0, 0);
+    }
+    __syncthreads();  // (A) pooling of the previous pair has finished reading the conv ring
+    // conv rows -> conv ring (fp16, bias + ReLU; rows above the image are 0, which
+    // equals max-pool's -inf padding because every window keeps >= 1 real value >= 0)
+    {
+      const int r = r0 + hr;
+      char* cr = crow + ((r + 6) % 3) * CROWB;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int wo = wo0 + tm * 16 + r16;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          half4 h;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) h[e] = r >= 0 ? (_Float16)fmaxf(acc[tm][tn][e] + bv[tn][e], 0.f) : (_Float16)0.f;
+          const int c = tn * 16 + q * 4;
+          *reinterpret_cast<half4*>(cr + crow_swz(wo, c >> 3) + (c & 7) * 2) = h;
+        }
+      }
+    }
+    if (j < PB && tid < 256) store_rows(hs + 9, nv);
+    __syncthreads();  // (B) conv rows + next input rows visible
+    if (j >= 1) {
+      // pooled row p = p0 + j - 1 from conv rows 2p-1, 2p, 2p+1 (= r0-1, r0, r0+1)
+      const int p = p0 + j - 1;
+      const int qc = tid >> 3, c8 = tid & 7;
+      float m[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = 0.f;
+#pragma unroll
+      for (int dr = -1; dr <= 1; ++dr) {
+        const char* cr = crow + ((2 * p + dr + 6) % 3) * CROWB;
+#pragma unroll
+        for (int dc = -1; dc <= 1; ++dc) {
+          const int wc = 2 * qc + dc;
+          if (wc < 0) continue;
+          half8 h = *reinterpret_cast<const half8*>(cr + crow_swz(wc, c8));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)h[e]);
+        }
+      }
+      half8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (_Float16)m[e];
+      *reinterpret_cast<half8*>(out + (((size_t)n * 64 + p) * 64 + qc) * 64 + c8 * 8) = o;
+    }
+  }
+}
+
+int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,
+                          hipStream_t s) {
+  PA_CHECK(Cin >= 1 && Cin <= 4, "stem: Cin %d", Cin);
+  if (B <= 0) return PA_OK;
+  hipLaunchKernelGGL(stem_pool_fp16, dim3(64 / stem::PB, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+}  // namespace pa

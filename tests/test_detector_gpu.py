@@ -134,6 +134,9 @@ def test_profile_reports_every_kernel():
     x = torch.from_numpy(synth.synthetic_frames(0, 8)).cuda()
     prof, y = m.profile(x)
     names = [n for n, _ in prof]
-    assert names[0] == "stem_conv7x7" and names[-1] == "avgpool_fc"
-    assert len(names) == 2 + 4 + 5 + 5 + 5 + 1
+    assert names[0] == "stem_conv7x7_pool" and names[-1] == "avgpool_fc"  # fp16: stem + maxpool fused
+    assert len(names) == 1 + 4 + 5 + 5 + 5 + 1
     assert torch.equal(y, m(x))
+    m.precision = "fp32"
+    prof32, _ = m.profile(x)
+    assert [n for n, _ in prof32][:2] == ["stem_conv7x7", "maxpool"]
