@@ -74,6 +74,11 @@ int pa_detector_forward(pa_detector* d, const float* x_dev, int B, float* y_dev,
 int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream,
                         float* ms_out, const char** names_out, int max_n);
 
+/* Tuning hook for interleaved A/B timing (tools/layer_ab.py): selects kernel
+ * variant `variant` for layer 1..4 (stage) or 0 (stem); 0 = the shipped choice.
+ * Process-global; not thread-safe; never needed in production. */
+int pa_debug_set_variant(int layer, int variant);
+
 /* Algorithmic FLOPs of one frame's forward (2 x MAC over the 20 convs + fc). */
 double pa_detector_flops_per_frame(const pa_detector* d);
 

@@ -7,6 +7,8 @@ namespace pa {
 
 enum { EPI_RELU = 1, EPI_RES = 2 };
 
+extern int g_variant[8];  // kernel-variant selector per layer (A/B timing; 0 = shipped)
+
 struct ConvArgs {
   const void* in;     // NHWC [B][Hin][Win][Cin]
   const void* w;      // [Cout][KS][KS][Cin], BatchNorm folded
@@ -21,6 +23,9 @@ int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);
 
 template <typename T>
 int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname);
+
+template <typename T>
+int launch_conv3x3_pipe(const ConvArgs& a, int variant, hipStream_t s);
 
 template <typename T>
 int launch_stem(const float* x, int B, int Cin, const T* w, const float* bias, T* out, hipStream_t s);

@@ -456,28 +456,55 @@ int launch_maxpool(const T* in, int B, int H, int W, int C, T* out, hipStream_t 
 
 // -------------------------------------------------------- avgpool + fc head
 // AdaptiveAvgPool2d((1,1)) + flatten + Linear(512, 2K) (models.py:31-32).
-// One workgroup per frame; thread t owns channels 2t, 2t+1.
+// One workgroup per frame.  Thread t reads 8-channel chunks of pixel group t/64
+// (a wave-instruction reads one contiguous pixel row, every thread has HW/4
+// independent loads); the 4 group sums are combined in a fixed order through LDS
+// (bit-reproducible), then the fc dot products are reduced across the workgroup.
 template <typename T>
 __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ in, int HW, int C,
                                                    const float* __restrict__ fcw, const float* __restrict__ fcb,
                                                    int nout, float* __restrict__ y) {
+  __shared__ float csum[4][512];
   __shared__ float part[4][32];
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const T* p = in + (size_t)n * HW * C;
-  float s0 = 0.f, s1 = 0.f;
-  const int c = 2 * tid;
-  if (c < C) {
-    for (int i = 0; i < HW; ++i) {
-      s0 += (float)p[(size_t)i * C + c];
-      s1 += (float)p[(size_t)i * C + c + 1];
+  const int C8 = C / 8;  // 16-B chunks per pixel (fp16) / 32-B (f32)
+  // thread -> (pixel group g = tid / C8, chunk c8 = tid % C8); 256 / C8 pixel groups
+  const int groups = 256 / C8;
+  const int g = tid / C8, c8 = tid - (tid / C8) * C8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (g < groups) {
+    // HW = 64 for 256x256 inputs: 16 pixels per thread, all loads issued before the adds
+    int px = g;
+    for (; px + 7 * groups < HW; px += 8 * groups) {
+      float v[8][8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) load8(p + (size_t)(px + u * groups) * C + c8 * 8, v[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += v[u][e];
     }
+    for (; px < HW; px += groups) {
+      float v[8];
+      load8(p + (size_t)px * C + c8 * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[g][c8 * 8 + e] = s[e];  // fixed order: deterministic
   }
+  __syncthreads();
   const float inv = 1.0f / (float)HW;
-  s0 *= inv;
-  s1 *= inv;
+  const int c = 2 * tid;
+  float m0 = 0.f, m1 = 0.f;
+  if (c < C) {
+    m0 = (csum[0][c] + csum[1][c] + csum[2][c] + csum[3][c]) * inv;
+    m1 = (csum[0][c + 1] + csum[1][c + 1] + csum[2][c + 1] + csum[3][c + 1]) * inv;
+  }
   for (int j = 0; j < nout; ++j) {
     float v = 0.f;
-    if (c < C) v = fcw[(size_t)j * C + c] * s0 + fcw[(size_t)j * C + c + 1] * s1;
+    if (c < C) v = fcw[(size_t)j * C + c] * m0 + fcw[(size_t)j * C + c + 1] * m1;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if (lane == 0) part[wid][j] = v;
@@ -489,7 +516,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ in, int
 template <typename T>
 int launch_head(const T* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
                 hipStream_t s) {
-  PA_CHECK(C <= 512 && C % 2 == 0 && nout <= 32, "head: C=%d nout=%d", C, nout);
+  PA_CHECK(C == 512 && nout <= 32, "head: C=%d nout=%d", C, nout);  // 4 pixel groups x 64 chunks
   if (B <= 0) return PA_OK;
   hipLaunchKernelGGL(head_kernel<T>, dim3(B), dim3(256), 0, s, in, HW, C, fcw, fcb, nout, y);
   PA_LAUNCH_CHECK();

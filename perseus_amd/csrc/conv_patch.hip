@@ -87,13 +87,16 @@ __device__ __forceinline__ int frag_off(int r) { return r < 4 ? 2 * r : (r < 12 
 template <int V>
 using ic = std::integral_constant<int, V>;
 
-template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int EPI>
+template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int EPI, int SB, int TPS,
+          int WD>
 __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   constexpr int NT = WM * WN * 64;
   constexpr int KB = PElem<T>::KB;
   constexpr int CPR = 16 / sizeof(T);
   constexpr int NCB = CIN / KB;  // 128-byte channel blocks
-  constexpr int NSTEPS = NCB * 9;
+  constexpr int SPC = 9 / TPS;   // steps per channel block (TPS taps per step)
+  constexpr int NSTEPS = NCB * SPC;
+  static_assert(TPS == 1 || TPS == 3, "taps per step");
   constexpr int KTOT = 9 * CIN;
   constexpr int PH = TH + 2, PW = TW + 2;
   // per-image patch stride in pixels; for 8-wide tiles a fragment pairs one row of
@@ -104,13 +107,14 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int PCH = (NP * 8 + NT - 1) / NT;  // patch 16-B chunks per thread
-  constexpr int BCH = BN * 8 / NT;             // weight chunks per thread
-  static_assert(BN * 8 % NT == 0, "weight tile / threads");
+  constexpr int BCH = TPS * BN * 8 / NT;       // weight chunks per thread
+  static_assert(TPS * BN * 8 % NT == 0, "weight tile / threads");
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
   static_assert(TW >= 16 || (TW == 8 && NI == 2), "fragment geometry");
   static_assert(PBUF == 2 || NCB == 1 || true, "");
   constexpr int PATCHB = NP * 128;
-  constexpr int WB = BN * 128;
+  constexpr int WB1 = BN * 128;  // one tap's weight tile
+  constexpr int WB = TPS * WB1;
   __shared__ __attribute__((aligned(16))) char smem[PBUF * PATCHB + 2 * WB];
   char* patch = smem;
   char* wbuf = smem + PBUF * PATCHB;
@@ -136,7 +140,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
 
   // ---- staging (register-staged; hipcc counts these loads itself)
   u32x4 rp[PCH];
-  u32x4 rb[3][BCH];
+  static_assert(SPC % WD == 0, "register-set rotation must be static");
+  u32x4 rb[WD][BCH];
   auto load_patch = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PCH; ++i) {
@@ -162,11 +167,13 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   };
   auto load_w = [&](int s, auto setc) __attribute__((always_inline)) {
     constexpr int SET = decltype(setc)::value;
-    const int cb = s / 9, tap = s - (s / 9) * 9;
+    const int cb = s / SPC, st = s - (s / SPC) * SPC;
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * NT;
-      const int row = c >> 3, ch = c & 7;
+      const int kc = c / (BN * 8), cc = c - (c / (BN * 8)) * (BN * 8);
+      const int row = cc >> 3, ch = cc & 7;
+      const int tap = st * TPS + kc;
       rb[SET][i] = *reinterpret_cast<const u32x4*>(w + (size_t)(n0 + row) * KTOT + tap * Cin + cb * KB + ch * CPR);
     }
   };
@@ -175,7 +182,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * NT;
-      *reinterpret_cast<u32x4*>(wbuf + buf * WB + pswz(c >> 3, c & 7)) = rb[SET][i];
+      const int kc = c / (BN * 8), cc = c - (c / (BN * 8)) * (BN * 8);
+      *reinterpret_cast<u32x4*>(wbuf + buf * WB + kc * WB1 + pswz(cc >> 3, cc & 7)) = rb[SET][i];
     }
   };
 
@@ -206,38 +214,53 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   store_patch(0);
   store_w(0, ic<0>{});
   load_w(NSTEPS > 1 ? 1 : 0, ic<1>{});
-  load_w(NSTEPS > 2 ? 2 : 0, ic<2>{});
+  load_w(NSTEPS > 2 ? 2 : 0, ic<2 % WD>{});
+  if constexpr (WD == 9) {
+    load_w(NSTEPS > 3 ? 3 : 0, ic<3 % WD>{});
+    load_w(NSTEPS > 4 ? 4 : 0, ic<4 % WD>{});
+    load_w(NSTEPS > 5 ? 5 : 0, ic<5 % WD>{});
+    load_w(NSTEPS > 6 ? 6 : 0, ic<6 % WD>{});
+    load_w(NSTEPS > 7 ? 7 : 0, ic<7 % WD>{});
+    load_w(NSTEPS > 8 ? 8 : 0, ic<8 % WD>{});
+  }
   __syncthreads();
 
-  // One K-step (cb, TAP): refill register set TAP%3 with W(s+3), MFMAs on the
-  // staged W(s) and patch(cb), then W(s+1) (set (TAP+1)%3) -> the other LDS
-  // buffer.  Weight loads stay in flight for ~2 steps; the next block's patch
-  // for the whole channel block.  Every load/store is unconditional (indices are
-  // clamped) so that hipcc's vmcnt bookkeeping stays exact.
-  auto step = [&](int cb, auto tapc) __attribute__((always_inline)) {
-    constexpr int TAP = decltype(tapc)::value;
-    constexpr int KR = TAP / 3, KC = TAP % 3;
-    const int s = cb * 9 + TAP;
-    load_w(s + 3 < NSTEPS ? s + 3 : NSTEPS - 1, ic<TAP % 3>{});
-    if constexpr (TAP == 0 && NCB > 1) load_patch(cb + 1 < NCB ? cb + 1 : NCB - 1);
+  // One K-step (cb, ST): TPS filter taps.  Refill register set ST%3 with W(s+3),
+  // MFMAs on the staged W(s) and patch(cb), then W(s+1) (set (ST+1)%3) -> the
+  // other LDS buffer.  Weight loads stay in flight for ~2 steps, the next block's
+  // patch for the whole channel block.  Every load/store is unconditional
+  // (indices are clamped) so that hipcc's vmcnt bookkeeping stays exact.
+  auto step = [&](int cb, auto stc) __attribute__((always_inline)) {
+    constexpr int ST = decltype(stc)::value;
+    const int s = cb * SPC + ST;
+    load_w(s + WD < NSTEPS ? s + WD : NSTEPS - 1, ic<ST % WD>{});
+    if constexpr (ST == 0 && NCB > 1) load_patch(cb + 1 < NCB ? cb + 1 : NCB - 1);
     const char* pb = patch + (PBUF == 2 ? (cb & 1) * PATCHB : 0);
     const char* wb = wbuf + (s & 1) * WB;
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      u32x4 fa[TN], fb[TM];
+    for (int kc = 0; kc < TPS; ++kc) {
+      const int tap = ST * TPS + kc;
+      const int toff = (tap / 3) * PW + (tap % 3);
+      u32x4 fa[2][TN], fb[2][TM];
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn)
-        fa[tn] = *reinterpret_cast<const u32x4*>(wb + pswz(wn * WTN + tn * 16 + r16, g * 4 + q));
+      for (int g = 0; g < 2; ++g) {
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-        fb[tm] = *reinterpret_cast<const u32x4*>(pb + pswz(ppix[tm] + KR * PW + KC, g * 4 + q));
+        for (int tn = 0; tn < TN; ++tn)
+          fa[g][tn] = *reinterpret_cast<const u32x4*>(wb + kc * WB1 + pswz(wn * WTN + tn * 16 + r16, g * 4 + q));
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
+        for (int tm = 0; tm < TM; ++tm)
+          fb[g][tm] = *reinterpret_cast<const u32x4*>(pb + pswz(ppix[tm] + toff, g * 4 + q));
+      }
+      if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn) pmma<T>(acc[tm][tn], fa[tn], fb[tm]);
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn) pmma<T>(acc[tm][tn], fa[g][tn], fb[g][tm]);
     }
-    store_w((s + 1) & 1, ic<(TAP + 1) % 3>{});
-    if constexpr (NCB > 1 && TAP == 8) {
+    store_w((s + 1) & 1, ic<(ST + 1) % WD>{});
+    if constexpr (NCB > 1 && ST == SPC - 1) {
       if constexpr (PBUF == 2) {
         store_patch((cb + 1) & 1);
         __syncthreads();
@@ -251,15 +274,21 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
     }
   };
   for (int cb = 0; cb < NCB; ++cb) {
-    step(cb, ic<0>{});
-    step(cb, ic<1>{});
-    step(cb, ic<2>{});
-    step(cb, ic<3>{});
-    step(cb, ic<4>{});
-    step(cb, ic<5>{});
-    step(cb, ic<6>{});
-    step(cb, ic<7>{});
-    step(cb, ic<8>{});
+    if constexpr (TPS == 3) {
+      step(cb, ic<0>{});
+      step(cb, ic<1>{});
+      step(cb, ic<2>{});
+    } else {
+      step(cb, ic<0>{});
+      step(cb, ic<1>{});
+      step(cb, ic<2>{});
+      step(cb, ic<3>{});
+      step(cb, ic<4>{});
+      step(cb, ic<5>{});
+      step(cb, ic<6>{});
+      step(cb, ic<7>{});
+      step(cb, ic<8>{});
+    }
   }
 
   // ---- epilogue straight from registers: lane holds channels co..co+3 of one pixel.
@@ -312,7 +341,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   }
 }
 
-template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN>
+template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int SB = 0, int TPS = 1,
+          int WD = 3>
 static int run_patch(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "patch conv: epilogue %d", a.epi);
   PA_CHECK(a.Cin == CIN, "patch conv: Cin %d != %d", a.Cin, CIN);
@@ -320,36 +350,81 @@ static int run_patch(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.Cout % BN == 0, "patch conv: Cout %d %% BN %d", a.Cout, BN);
   const int tiles = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW) * (a.Cout / BN);
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES>), dim3(tiles),
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES, SB, TPS, WD>), dim3(tiles),
                        dim3(WM * WN * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU>), dim3(tiles),
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU, SB, TPS, WD>), dim3(tiles),
                        dim3(WM * WN * 64), 0, s, a);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
 
-// Stride-1 3x3 conv, Hin == Hout.  Tile configuration per feature-map size.
+// Stride-1 3x3 conv, Hin == Hout.  Tile configuration per feature-map size;
+// g_variant[layer] (pa_debug_set_variant) selects alternatives for A/B timing.
+int g_variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
 template <typename T>
 int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
   PA_CHECK(a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout, "patch conv: stride-1 only");
   PA_CHECK(a.Cin % PElem<T>::KB == 0, "patch conv: Cin %d", a.Cin);
   if (a.B <= 0) return PA_OK;
+  {
+    const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : 4;
+    if (g_variant[layer] >= 10) {
+      static const char* names[5] = {"", "conv3x3q_l1", "conv3x3q_l2", "conv3x3q_l3", "conv3x3q_l4"};
+      if (kname) *kname = names[layer];
+      return launch_conv3x3_pipe<T>(a, g_variant[layer] - 10, s);
+    }
+  }
   if (a.Hout == 64 && a.Cout == 64) {
     if (kname) *kname = "conv3x3p_l1";
-    return run_patch<T, 16, 32, 1, 64, 8, 1, 1, 64>(a, s);
+    switch (g_variant[1]) {
+      case 1: return run_patch<T, 16, 32, 1, 64, 8, 1, 1, 64, 1>(a, s);
+      case 2: return run_patch<T, 16, 32, 1, 64, 4, 1, 1, 64, 1>(a, s);
+      case 3: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0>(a, s);
+      case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 0>(a, s);
+      case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0, 1, 9>(a, s);
+      case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 0, 1, 9>(a, s);
+      case 7: return run_patch<T, 16, 32, 1, 64, 8, 1, 1, 64, 0>(a, s);
+      default: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0>(a, s);
+    }
   }
   if (a.Hout == 32) {
     if (kname) *kname = "conv3x3p_l2";
-    return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128>(a, s);
+    switch (g_variant[2]) {
+      case 1: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 128, 1>(a, s);
+      case 2: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 128, 1>(a, s);
+      case 3: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 128, 0>(a, s);
+      case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 128, 0>(a, s);
+      case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 128, 0, 1, 9>(a, s);
+      case 6: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0, 1, 9>(a, s);
+      default: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0>(a, s);
+    }
   }
   if (a.Hout == 16) {
     if (kname) *kname = "conv3x3p_l3";
-    return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256>(a, s);
+    switch (g_variant[3]) {
+      case 1: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 1>(a, s);
+      case 2: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 256, 1>(a, s);
+      case 3: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 256, 0>(a, s);
+      case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 256, 0>(a, s);
+      case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 256, 0, 1, 9>(a, s);
+      case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 256, 0, 1, 9>(a, s);
+      default: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 0>(a, s);
+    }
   }
   if (a.Hout == 8) {
     if (kname) *kname = "conv3x3p_l4";
-    return run_patch<T, 8, 8, 2, 64, 2, 2, 2, 512>(a, s);
+    switch (g_variant[4]) {
+      case 1: return run_patch<T, 8, 8, 2, 64, 2, 2, 2, 512, 1>(a, s);
+      case 2: return run_patch<T, 8, 8, 2, 64, 4, 2, 2, 512, 0>(a, s);
+      case 3: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0>(a, s);
+      case 4: return run_patch<T, 8, 8, 2, 32, 2, 2, 1, 512, 0>(a, s);
+      case 5: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0, 1, 9>(a, s);
+      case 6: return run_patch<T, 8, 8, 2, 64, 2, 2, 1, 512, 0, 1, 9>(a, s);
+      case 7: return run_patch<T, 8, 8, 2, 64, 2, 2, 2, 512, 0>(a, s);
+      default: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0>(a, s);
+    }
   }
   set_error("patch conv: no configuration for %dx%d", a.Hout, a.Wout);
   return PA_EINVAL;

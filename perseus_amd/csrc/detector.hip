@@ -394,6 +394,12 @@ int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev,
   return rc == PA_OK ? n : rc;
 }
 
+int pa_debug_set_variant(int layer, int variant) {
+  PA_CHECK(layer >= 0 && layer < 8 && variant >= 0, "layer %d variant %d", layer, variant);
+  pa::g_variant[layer] = variant;
+  return PA_OK;
+}
+
 double pa_detector_flops_per_frame(const pa_detector* d) { return d ? d->flops_per_frame : 0.0; }
 
 int pa_preprocess_rgbd(const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws, int bgr, float near_m,

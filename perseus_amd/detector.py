@@ -183,7 +183,7 @@ class KeypointCNN(nn.Module):
         L = _lib.lib()
         _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP32 if self.precision == "fp32" else _lib.PREC_FP16),
                    "set_precision")
-        y = torch.empty((x.shape[0], 2 * self.n_keypoints), dtype=torch.float32, device=dev)
+        y = torch.full((x.shape[0], 2 * self.n_keypoints), float("nan"), dtype=torch.float32, device=dev)
         ms = (_lib.C.c_float * max_kernels)()
         names = (_lib.C.c_char_p * max_kernels)()
         with torch.cuda.device(dev):
