@@ -142,7 +142,7 @@ def main():
     return line
 
 
-def conv_flops(B, fused_stem=True):
+def conv_flops(B, fused_stem=True, fused_ds=True):
     """Algorithmic FLOPs per launch, in forward order (matches pa_detector_profile)."""
     stem = 2.0 * B * 128 * 128 * 64 * 49 * 4  # true K = 196
     fl = [stem] if fused_stem else [stem, 0.0]  # fp16 fuses conv7x7 + maxpool
@@ -152,9 +152,12 @@ def conv_flops(B, fused_stem=True):
             s = 2 if (li > 0 and bi == 0) else 1
             ho = hw // s
             c_in = cin if bi == 0 else cout
-            fl.append(2.0 * B * ho * ho * cout * 9 * c_in)          # conv1
+            c1 = 2.0 * B * ho * ho * cout * 9 * c_in
             if bi == 0 and li > 0:
-                fl.append(2.0 * B * ho * ho * cout * c_in)          # downsample
+                ds = 2.0 * B * ho * ho * cout * c_in
+                fl += [c1 + ds] if fused_ds else [c1, ds]  # conv1 s2 (+ fused 1x1 s2 downsample)
+            else:
+                fl.append(c1)
             fl.append(2.0 * B * ho * ho * cout * 9 * cout)          # conv2
             hw = ho
         cin = cout
@@ -163,8 +166,16 @@ def conv_flops(B, fused_stem=True):
 
 
 def roofline(per_launch, B, precision):
-    fl = conv_flops(B, fused_stem=len(per_launch) == 21)
-    if len(fl) != len(per_launch):
+    fl = None
+    for fs in (True, False):
+        for fd in (True, False):
+            c = conv_flops(B, fused_stem=fs, fused_ds=fd)
+            if len(c) == len(per_launch):
+                fl = c
+                break
+        if fl:
+            break
+    if fl is None:
         return None
     groups = {}
     for (idx, name, ms), f in zip(per_launch, fl):

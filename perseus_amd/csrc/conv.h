@@ -18,6 +18,21 @@ struct ConvArgs {
   int B, Hin, Win, Cin, Hout, Wout, Cout, stride, pad, epi, M;
 };
 
+// conv3x3 s2 (+bn, relu) -> out and 1x1 s2 downsample (+bn) -> out2, one pass
+struct ConvS2Args {
+  const void* in;      // NHWC [B][Hin][Win][Cin]
+  const void* w;       // [Cout][3][3][Cin]
+  const float* bias;   // [Cout]
+  const void* wds;     // [Cout][Cin]
+  const float* bias2;  // [Cout]
+  void* out;           // NHWC [B][Hout][Wout][Cout]
+  void* out2;          // NHWC [B][Hout][Wout][Cout]
+  int B, Hin, Win, Cin, Hout, Wout, Cout;
+};
+
+template <typename T>
+int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname);
+
 template <typename T>
 int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);
 

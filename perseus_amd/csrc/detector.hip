@@ -232,36 +232,60 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     a.Hout = ho;
     a.Wout = ho;
     a.M = B * ho * ho;
-    // conv1 + bn1 + relu
-    a.in = X;
-    a.w = wts + c1.w_off;
-    a.bias = d->bias + c1.b_off;
-    a.res = nullptr;
-    a.out = Tb;
-    a.Cin = c1.cin;
-    a.Cout = c1.cout;
-    a.stride = c1.stride;
-    a.pad = 1;
-    a.epi = EPI_RELU;
-    if (c1.stride == 1)
-      PA_TRY(launch_conv3x3_s1<T>(a, s, &kn));
-    else
-      PA_TRY(launch_conv<T>(a, 3, s, &kn));
-    if (prof) prof->mark(kn);
     const T* res = X;
     T* out = X;  // identity block: residual add in place (same element, same thread)
-    if (b.ds >= 0) {
+    if (b.ds >= 0 && g_variant[5] == 0) {
+      // conv1 3x3 s2 + bn1 + relu and downsample 1x1 s2 + bn in one pass over X
       const ConvL& cd = d->convs[b.ds];
-      ConvArgs dsa = a;
-      dsa.w = wts + cd.w_off;
-      dsa.bias = d->bias + cd.b_off;
-      dsa.out = D;
-      dsa.pad = 0;
-      dsa.epi = 0;
-      PA_TRY(launch_conv<T>(dsa, 1, s, &kn));
+      ConvS2Args sa{};
+      sa.in = X;
+      sa.w = wts + c1.w_off;
+      sa.bias = d->bias + c1.b_off;
+      sa.wds = wts + cd.w_off;
+      sa.bias2 = d->bias + cd.b_off;
+      sa.out = Tb;
+      sa.out2 = D;
+      sa.B = B;
+      sa.Hin = hw;
+      sa.Win = hw;
+      sa.Cin = c1.cin;
+      sa.Hout = ho;
+      sa.Wout = ho;
+      sa.Cout = c1.cout;
+      PA_TRY(launch_conv3x3s2_ds<T>(sa, s, &kn));
       if (prof) prof->mark(kn);
       res = D;
       out = D;
+    } else {
+      // conv1 + bn1 + relu
+      a.in = X;
+      a.w = wts + c1.w_off;
+      a.bias = d->bias + c1.b_off;
+      a.res = nullptr;
+      a.out = Tb;
+      a.Cin = c1.cin;
+      a.Cout = c1.cout;
+      a.stride = c1.stride;
+      a.pad = 1;
+      a.epi = EPI_RELU;
+      if (c1.stride == 1)
+        PA_TRY(launch_conv3x3_s1<T>(a, s, &kn));
+      else
+        PA_TRY(launch_conv<T>(a, 3, s, &kn));
+      if (prof) prof->mark(kn);
+      if (b.ds >= 0) {
+        const ConvL& cd = d->convs[b.ds];
+        ConvArgs dsa = a;
+        dsa.w = wts + cd.w_off;
+        dsa.bias = d->bias + cd.b_off;
+        dsa.out = D;
+        dsa.pad = 0;
+        dsa.epi = 0;
+        PA_TRY(launch_conv<T>(dsa, 1, s, &kn));
+        if (prof) prof->mark(kn);
+        res = D;
+        out = D;
+      }
     }
     // conv2 + bn2 + residual + relu
     ConvArgs b2{};

@@ -135,7 +135,8 @@ def test_profile_reports_every_kernel():
     prof, y = m.profile(x)
     names = [n for n, _ in prof]
     assert names[0] == "stem_conv7x7_pool" and names[-1] == "avgpool_fc"  # fp16: stem + maxpool fused
-    assert len(names) == 1 + 4 + 5 + 5 + 5 + 1
+    assert len(names) == 1 + 4 + 4 + 4 + 4 + 1  # stride-2 conv1 + 1x1 downsample fused
+    assert names[5].startswith("conv3x3s2ds")
     assert torch.equal(y, m(x))
     m.precision = "fp32"
     prof32, _ = m.profile(x)
