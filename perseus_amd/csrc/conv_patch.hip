@@ -88,7 +88,7 @@ template <int V>
 using ic = std::integral_constant<int, V>;
 
 template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int EPI, int SB, int TPS,
-          int WD>
+          int WD, int ABL = 0>
 __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   constexpr int NT = WM * WN * 64;
   constexpr int KB = PElem<T>::KB;
@@ -225,6 +225,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   }
   __syncthreads();
 
+  u32x4 fa0[2][TN], fb0[2][TM];  // ablation (ABL >= 2): fragments reused from step 0
   // One K-step (cb, ST): TPS filter taps.  Refill register set ST%3 with W(s+3),
   // MFMAs on the staged W(s) and patch(cb), then W(s+1) (set (ST+1)%3) -> the
   // other LDS buffer.  Weight loads stay in flight for ~2 steps, the next block's
@@ -233,8 +234,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   auto step = [&](int cb, auto stc) __attribute__((always_inline)) {
     constexpr int ST = decltype(stc)::value;
     const int s = cb * SPC + ST;
-    load_w(s + WD < NSTEPS ? s + WD : NSTEPS - 1, ic<ST % WD>{});
-    if constexpr (ST == 0 && NCB > 1) load_patch(cb + 1 < NCB ? cb + 1 : NCB - 1);
+    if constexpr (ABL == 0) load_w(s + WD < NSTEPS ? s + WD : NSTEPS - 1, ic<ST % WD>{});
+    if constexpr (ST == 0 && NCB > 1 && ABL == 0) load_patch(cb + 1 < NCB ? cb + 1 : NCB - 1);
     const char* pb = patch + (PBUF == 2 ? (cb & 1) * PATCHB : 0);
     const char* wb = wbuf + (s & 1) * WB;
 #pragma unroll
@@ -244,6 +245,15 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
       u32x4 fa[2][TN], fb[2][TM];
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
+        if constexpr (ABL >= 2) {
+          if (s > 0) {
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) fa[g][tn] = fa0[g][tn];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) fb[g][tm] = fb0[g][tm];
+            continue;
+          }
+        }
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
           fa[g][tn] = *reinterpret_cast<const u32x4*>(wb + kc * WB1 + pswz(wn * WTN + tn * 16 + r16, g * 4 + q));
@@ -258,9 +268,20 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
           for (int tn = 0; tn < TN; ++tn) pmma<T>(acc[tm][tn], fa[g][tn], fb[g][tm]);
+      if constexpr (ABL >= 2) {
+        if (s == 0) {
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) fa0[g][tn] = fa[g][tn];
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) fb0[g][tm] = fb[g][tm];
+          }
+        }
+      }
     }
-    store_w((s + 1) & 1, ic<(ST + 1) % WD>{});
-    if constexpr (NCB > 1 && ST == SPC - 1) {
+    if constexpr (ABL == 0) store_w((s + 1) & 1, ic<(ST + 1) % WD>{});
+    if constexpr (NCB > 1 && ST == SPC - 1 && ABL == 0) {
       if constexpr (PBUF == 2) {
         store_patch((cb + 1) & 1);
         __syncthreads();
@@ -342,7 +363,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
 }
 
 template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int SB = 0, int TPS = 1,
-          int WD = 3>
+          int WD = 3, int ABL = 0>
 static int run_patch(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "patch conv: epilogue %d", a.epi);
   PA_CHECK(a.Cin == CIN, "patch conv: Cin %d != %d", a.Cin, CIN);
@@ -350,10 +371,10 @@ static int run_patch(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.Cout % BN == 0, "patch conv: Cout %d %% BN %d", a.Cout, BN);
   const int tiles = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW) * (a.Cout / BN);
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES, SB, TPS, WD>), dim3(tiles),
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES, SB, TPS, WD, ABL>), dim3(tiles),
                        dim3(WM * WN * 64), 0, s, a);
   else
-    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU, SB, TPS, WD>), dim3(tiles),
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU, SB, TPS, WD, ABL>), dim3(tiles),
                        dim3(WM * WN * 64), 0, s, a);
   PA_LAUNCH_CHECK();
   return PA_OK;
@@ -386,6 +407,8 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0, 1, 9>(a, s);
       case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 0, 1, 9>(a, s);
       case 7: return run_patch<T, 16, 32, 1, 64, 8, 1, 1, 64, 0>(a, s);
+      case 20: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0, 1, 3, 1>(a, s);
+      case 21: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0, 1, 3, 2>(a, s);
       default: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0>(a, s);
     }
   }
@@ -398,6 +421,8 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 128, 0>(a, s);
       case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 128, 0, 1, 9>(a, s);
       case 6: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0, 1, 9>(a, s);
+      case 20: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0, 1, 3, 1>(a, s);
+      case 21: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0, 1, 3, 2>(a, s);
       default: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0>(a, s);
     }
   }
@@ -410,6 +435,8 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 256, 0>(a, s);
       case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 256, 0, 1, 9>(a, s);
       case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 256, 0, 1, 9>(a, s);
+      case 20: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 0, 1, 3, 1>(a, s);
+      case 21: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 0, 1, 3, 2>(a, s);
       default: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 0>(a, s);
     }
   }
@@ -423,6 +450,8 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 5: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0, 1, 9>(a, s);
       case 6: return run_patch<T, 8, 8, 2, 64, 2, 2, 1, 512, 0, 1, 9>(a, s);
       case 7: return run_patch<T, 8, 8, 2, 64, 2, 2, 2, 512, 0>(a, s);
+      case 20: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0, 1, 3, 1>(a, s);
+      case 21: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0, 1, 3, 2>(a, s);
       default: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0>(a, s);
     }
   }
