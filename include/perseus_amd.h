@@ -125,6 +125,37 @@ int pa_dyn_linearize(int n, const double* t1_dev, const double* w_dev, const dou
 int pa_cv_linearize(int n, const double* v1_dev, const double* v2_dev, const double* inv_sigma_dev,
                     double* r_dev, double* j0_dev, double* j1_dev, double* err_dev, void* stream);
 
+/* Config 3: every factor of T trajectories x L frames in ONE launch,
+ * keypoint measurements taken straight from the detector output y (B = T*L rows of
+ * 2K normalized coordinates, denormalized on device as validate.py:144-153 does).
+ * Per frame f (= t*L + l): K projection factors (corner k: p_b = corners[k], z =
+ * pixel k of frame f, body pose pose[f]); per consecutive pair (l, l+1) of a
+ * trajectory: one PoseDynamicsFactor (pose[f], angvel[f], vel[f], pose[f+1]) and
+ * one ConstantVelocityFactor (vel[f], vel[f+1]).  Outputs use the per-factor
+ * layouts of the batched entry points above; proj arrays have T*L*K rows, dyn
+ * and cv arrays T*(L-1).  inv_sigma / err / J / status pointers may be NULL. */
+typedef struct pa_traj_args {
+  int T, L, n_kp, H, W;
+  const float* y;          /* (T*L, 2K) normalized keypoints */
+  const double* pose;      /* (T*L, 12) */
+  const double* vel;       /* (T*L, 3) linear velocity (vel_frame) */
+  const double* angvel;    /* (T*L, 3) body angular velocity */
+  const double* corners;   /* (K, 3) body-frame keypoints */
+  const double* K;         /* (5) fx, fy, s, u0, v0 */
+  const double* tcam;      /* (12) camera pose or NULL = identity */
+  double dt;
+  int vel_frame;
+  const double* isig_proj; /* (2) or NULL */
+  const double* isig_dyn;  /* (6) or NULL */
+  const double* isig_cv;   /* (3) or NULL */
+  double *r_proj, *j_proj, *err_proj;
+  int32_t* status;
+  double *r_dyn, *j_dyn0, *j_dyn1, *j_dyn2, *j_dyn3, *err_dyn;
+  double *r_cv, *j_cv0, *j_cv1, *err_cv;
+} pa_traj_args;
+
+int pa_trajectory_linearize(const pa_traj_args* args, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,8 +21,22 @@ class PerseusError(RuntimeError):
     pass
 
 
+class TrajArgs(C.Structure):
+    """Mirror of `pa_traj_args` (include/perseus_amd.h)."""
+
+    _fields_ = [("T", C.c_int), ("L", C.c_int), ("n_kp", C.c_int), ("H", C.c_int), ("W", C.c_int),
+                ("y", C.c_void_p), ("pose", C.c_void_p), ("vel", C.c_void_p), ("angvel", C.c_void_p),
+                ("corners", C.c_void_p), ("K", C.c_void_p), ("tcam", C.c_void_p), ("dt", C.c_double),
+                ("vel_frame", C.c_int), ("isig_proj", C.c_void_p), ("isig_dyn", C.c_void_p),
+                ("isig_cv", C.c_void_p), ("r_proj", C.c_void_p), ("j_proj", C.c_void_p), ("err_proj", C.c_void_p),
+                ("status", C.c_void_p), ("r_dyn", C.c_void_p), ("j_dyn0", C.c_void_p), ("j_dyn1", C.c_void_p),
+                ("j_dyn2", C.c_void_p), ("j_dyn3", C.c_void_p), ("err_dyn", C.c_void_p), ("r_cv", C.c_void_p),
+                ("j_cv0", C.c_void_p), ("j_cv1", C.c_void_p), ("err_cv", C.c_void_p)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
+    "pa_trajectory_linearize": (C.c_int, [C.POINTER(TrajArgs), C.c_void_p]),
     "pa_last_error": (C.c_char_p, []),
     "pa_version": (C.c_char_p, []),
     "pa_detector_create": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -297,18 +297,16 @@ __device__ __forceinline__ void store_colmajor(double* J, const M6& m, int rows,
     for (int r = 0; r < 6; ++r) J[c * rows + r] = m(r, col0 + c) * (isig ? isig[r] : 1.0);
 }
 
-__global__ __launch_bounds__(64) void dyn_kernel(int n, const double* __restrict__ T1p, const double* __restrict__ wp,
-                                                 const double* __restrict__ vp, const double* __restrict__ T2p,
-                                                 double dt, int vel_frame, const double* __restrict__ isig,
-                                                 double* __restrict__ r_out, double* __restrict__ J0,
-                                                 double* __restrict__ J1, double* __restrict__ J2,
-                                                 double* __restrict__ J3, double* __restrict__ err) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n) return;
-  const Pose T1 = load_pose(T1p + (size_t)i * 12);
-  const Pose T2 = load_pose(T2p + (size_t)i * 12);
-  const V3 w = load3(wp + (size_t)i * 3);
-  V3 v = load3(vp + (size_t)i * 3);
+// One PoseDynamicsFactor: inputs point at this factor's records, outputs at its
+// slots (r 6, J0 36, J1 18, J2 18, J3 36 column-major; err 1; any J may be null).
+__device__ void dyn_one(const double* __restrict__ T1p, const double* __restrict__ wp, const double* __restrict__ vp,
+                        const double* __restrict__ T2p, double dt, int vel_frame, const double* __restrict__ isig,
+                        double* __restrict__ r_out, double* __restrict__ J0, double* __restrict__ J1,
+                        double* __restrict__ J2, double* __restrict__ J3, double* __restrict__ err) {
+  const Pose T1 = load_pose(T1p);
+  const Pose T2 = load_pose(T2p);
+  const V3 w = load3(wp);
+  V3 v = load3(vp);
   V3 vb = v;
   if (vel_frame == PA_VEL_WORLD) vb = mtv(T1.R, v);  // transformTo / unrotate (factors.py:100,134)
   const V3 xw = dt * w, xv = dt * vb;
@@ -322,12 +320,12 @@ __global__ __launch_bounds__(64) void dyn_kernel(int n, const double* __restrict
 #pragma unroll
   for (int k = 0; k < 6; ++k) rs[k] = r[k] * (isig ? isig[k] : 1.0);
 #pragma unroll
-  for (int k = 0; k < 6; ++k) r_out[(size_t)i * 6 + k] = rs[k];
+  for (int k = 0; k < 6; ++k) r_out[k] = rs[k];
   if (err) {
     double e = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) e += rs[k] * rs[k];
-    err[i] = 0.5 * e;
+    *err = 0.5 * e;
   }
   if (!(J0 || J1 || J2 || J3)) return;
   // dlog = LogmapDerivative(rel) (:112)
@@ -366,10 +364,45 @@ __global__ __launch_bounds__(64) void dyn_kernel(int n, const double* __restrict
 #pragma unroll
       for (int c = 0; c < 3; ++c) h2(r6, c) = dtw(r6, 3 + c);  // (:128)
   }
-  if (J0) store_colmajor(J0 + (size_t)i * 36, h0, 6, 0, 6, isig);
-  if (J1) store_colmajor(J1 + (size_t)i * 18, dtw, 6, 0, 3, isig);
-  if (J2) store_colmajor(J2 + (size_t)i * 18, h2, 6, 0, 3, isig);
-  if (J3) store_colmajor(J3 + (size_t)i * 36, dlog, 6, 0, 6, isig);  // dlog * I (:130)
+  if (J0) store_colmajor(J0, h0, 6, 0, 6, isig);
+  if (J1) store_colmajor(J1, dtw, 6, 0, 3, isig);
+  if (J2) store_colmajor(J2, h2, 6, 0, 3, isig);
+  if (J3) store_colmajor(J3, dlog, 6, 0, 6, isig);  // dlog * I (:130)
+}
+
+__global__ __launch_bounds__(64) void dyn_kernel(int n, const double* __restrict__ T1p, const double* __restrict__ wp,
+                                                 const double* __restrict__ vp, const double* __restrict__ T2p,
+                                                 double dt, int vel_frame, const double* __restrict__ isig,
+                                                 double* __restrict__ r_out, double* __restrict__ J0,
+                                                 double* __restrict__ J1, double* __restrict__ J2,
+                                                 double* __restrict__ J3, double* __restrict__ err) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const size_t u = i;
+  dyn_one(T1p + u * 12, wp + u * 3, vp + u * 3, T2p + u * 12, dt, vel_frame, isig, r_out + u * 6,
+          J0 ? J0 + u * 36 : nullptr, J1 ? J1 + u * 18 : nullptr, J2 ? J2 + u * 18 : nullptr,
+          J3 ? J3 + u * 36 : nullptr, err ? err + u : nullptr);
+}
+
+__device__ void cv_one(const double* __restrict__ v1, const double* __restrict__ v2, const double* __restrict__ isig,
+                       double* __restrict__ r, double* __restrict__ J0, double* __restrict__ J1,
+                       double* __restrict__ err) {
+  double e = 0.0;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double s = isig ? isig[k] : 1.0;
+    const double rk = (v2[k] - v1[k]) * s;
+    r[k] = rk;
+    e += rk * rk;
+  }
+  if (err) *err = 0.5 * e;
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+      const double s = isig ? isig[rr] : 1.0;
+      if (J0) J0[c * 3 + rr] = (rr == c ? -1.0 : 0.0) * s;
+      if (J1) J1[c * 3 + rr] = (rr == c ? 1.0 : 0.0) * s;
+    }
 }
 
 __global__ __launch_bounds__(64) void cv_kernel(int n, const double* __restrict__ v1, const double* __restrict__ v2,
@@ -378,39 +411,21 @@ __global__ __launch_bounds__(64) void cv_kernel(int n, const double* __restrict_
                                                 double* __restrict__ err) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= n) return;
-  double e = 0.0;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const double s = isig ? isig[k] : 1.0;
-    const double rk = (v2[(size_t)i * 3 + k] - v1[(size_t)i * 3 + k]) * s;
-    r[(size_t)i * 3 + k] = rk;
-    e += rk * rk;
-  }
-  if (err) err[i] = 0.5 * e;
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int rr = 0; rr < 3; ++rr) {
-      const double s = isig ? isig[rr] : 1.0;
-      if (J0) J0[(size_t)i * 9 + c * 3 + rr] = (rr == c ? -1.0 : 0.0) * s;
-      if (J1) J1[(size_t)i * 9 + c * 3 + rr] = (rr == c ? 1.0 : 0.0) * s;
-    }
+  const size_t u = i;
+  cv_one(v1 + u * 3, v2 + u * 3, isig, r + u * 3, J0 ? J0 + u * 9 : nullptr, J1 ? J1 + u * 9 : nullptr,
+         err ? err + u : nullptr);
 }
 
-__global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restrict__ Tb, const double* __restrict__ pbp,
-                                                  const double* __restrict__ zp, const double* __restrict__ Kp,
-                                                  int k_stride, const double* __restrict__ Tcp, int tc_stride,
-                                                  const double* __restrict__ isig, double* __restrict__ r_out,
-                                                  double* __restrict__ J, double* __restrict__ err,
-                                                  int32_t* __restrict__ status) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n) return;
-  const Pose T = load_pose(Tb + (size_t)i * 12);
-  const V3 pb = load3(pbp + (size_t)i * 3);
-  const double* K = Kp + (size_t)i * k_stride;
+// One KeypointProjectionFactor.  K: 5 values; Tc: 12 values or null (identity);
+// outputs r 2, J 12 (col-major 2x6) or null, err / status or null.
+__device__ void proj_one(const double* __restrict__ Tb, V3 pb, double zx, double zy, const double* __restrict__ K,
+                         const double* __restrict__ Tcp, const double* __restrict__ isig, double* __restrict__ r_out,
+                         double* __restrict__ J, double* __restrict__ err, int32_t* __restrict__ status) {
+  const Pose T = load_pose(Tb);
   const double fx = K[0], fy = K[1], sk = K[2], u0 = K[3], v0 = K[4];
   Pose C;
   if (Tcp) {
-    C = load_pose(Tcp + (size_t)i * tc_stride);
+    C = load_pose(Tcp);
   } else {
     C.R = eye3();
     C.t = v3(0, 0, 0);
@@ -422,22 +437,22 @@ __global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restric
   const double s0 = isig ? isig[0] : 1.0, s1 = isig ? isig[1] : 1.0;
   if (!(pc.z > 0.0)) {
     const double nan = __builtin_nan("");
-    r_out[(size_t)i * 2] = nan;
-    r_out[(size_t)i * 2 + 1] = nan;
+    r_out[0] = nan;
+    r_out[1] = nan;
     if (J)
-      for (int k = 0; k < 12; ++k) J[(size_t)i * 12 + k] = nan;
-    if (err) err[i] = nan;
-    if (status) status[i] = 1;
+      for (int k = 0; k < 12; ++k) J[k] = nan;
+    if (err) *err = nan;
+    if (status) *status = 1;
     return;
   }
   const double iz = 1.0 / pc.z;
   const double x = pc.x * iz, y = pc.y * iz;
   const double u = fx * x + sk * y + u0, v = fy * y + v0;
-  const double r0 = (u - zp[(size_t)i * 2]) * s0, r1 = (v - zp[(size_t)i * 2 + 1]) * s1;
-  r_out[(size_t)i * 2] = r0;
-  r_out[(size_t)i * 2 + 1] = r1;
-  if (err) err[i] = 0.5 * (r0 * r0 + r1 * r1);
-  if (status) status[i] = 0;
+  const double r0 = (u - zx) * s0, r1 = (v - zy) * s1;
+  r_out[0] = r0;
+  r_out[1] = r1;
+  if (err) *err = 0.5 * (r0 * r0 + r1 * r1);
+  if (status) *status = 0;
   if (!J) return;
   // dproj_dpoint = Dcal * Dpn * Rc^T (2x3), Dcal = [[fx, s],[0, fy]], Dpn = 1/z [[1,0,-x],[0,1,-y]]
   double Dpn[2][3] = {{iz, 0.0, -x * iz}, {0.0, iz, -y * iz}};
@@ -451,7 +466,6 @@ __global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restric
     for (int c = 0; c < 3; ++c) Dw[rr][c] = Dp[rr][0] * C.R(c, 0) + Dp[rr][1] * C.R(c, 1) + Dp[rr][2] * C.R(c, 2);
   // dpc_dpose = [R skew(-pb), R]
   const M3 RS = mul(T.R, skew(-1.0 * pb));
-  double* Jo = J + (size_t)i * 12;
   for (int c = 0; c < 6; ++c) {
     double h[2];
     for (int rr = 0; rr < 2; ++rr) {
@@ -459,8 +473,58 @@ __global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restric
       for (int k = 0; k < 3; ++k) s += Dw[rr][k] * (c < 3 ? RS(k, c) : T.R(k, c - 3));
       h[rr] = s;
     }
-    Jo[c * 2] = h[0] * s0;  // H0 = dproj_dpoint @ dpc_dpose (:264), column-major
-    Jo[c * 2 + 1] = h[1] * s1;
+    J[c * 2] = h[0] * s0;  // H0 = dproj_dpoint @ dpc_dpose (:264), column-major
+    J[c * 2 + 1] = h[1] * s1;
+  }
+}
+
+__global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restrict__ Tb, const double* __restrict__ pbp,
+                                                  const double* __restrict__ zp, const double* __restrict__ Kp,
+                                                  int k_stride, const double* __restrict__ Tcp, int tc_stride,
+                                                  const double* __restrict__ isig, double* __restrict__ r_out,
+                                                  double* __restrict__ J, double* __restrict__ err,
+                                                  int32_t* __restrict__ status) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const size_t u = i;
+  proj_one(Tb + u * 12, load3(pbp + u * 3), zp[u * 2], zp[u * 2 + 1], Kp + u * k_stride,
+           Tcp ? Tcp + u * tc_stride : nullptr, isig, r_out + u * 2, J ? J + u * 12 : nullptr, err ? err + u : nullptr,
+           status ? status + u : nullptr);
+}
+
+// Config 3: all factors of T trajectories x L frames in one launch, measurements
+// straight from the detector output y (normalized, denormalized here exactly as
+// kornia's denormalize_pixel_coordinates: px = (n + 1) (S - 1) / 2 in f32).
+// Thread index space: [proj: T*L*K | dyn: T*(L-1) | cv: T*(L-1)].
+__global__ __launch_bounds__(64) void traj_kernel(pa_traj_args a) {
+  const long i = blockIdx.x * 64L + threadIdx.x;
+  const long F = (long)a.T * a.L;
+  const long np = F * a.n_kp, nd = (long)a.T * (a.L - 1);
+  if (i < np) {
+    const long f = i / a.n_kp;
+    const int k = (int)(i - f * a.n_kp);
+    const float* yf = a.y + f * 2 * a.n_kp + 2 * k;
+    const float px = (yf[0] + 1.0f) * ((float)(a.W - 1) / 2.0f);
+    const float py = (yf[1] + 1.0f) * ((float)(a.H - 1) / 2.0f);
+    proj_one(a.pose + f * 12, load3(a.corners + 3 * k), (double)px, (double)py, a.K, a.tcam, a.isig_proj,
+             a.r_proj + i * 2, a.j_proj ? a.j_proj + i * 12 : nullptr, a.err_proj ? a.err_proj + i : nullptr,
+             a.status ? a.status + i : nullptr);
+    return;
+  }
+  const long jd = i - np;
+  if (jd < nd) {
+    const long t = jd / (a.L - 1), f = t * a.L + (jd - t * (a.L - 1));
+    dyn_one(a.pose + f * 12, a.angvel + f * 3, a.vel + f * 3, a.pose + (f + 1) * 12, a.dt, a.vel_frame, a.isig_dyn,
+            a.r_dyn + jd * 6, a.j_dyn0 ? a.j_dyn0 + jd * 36 : nullptr, a.j_dyn1 ? a.j_dyn1 + jd * 18 : nullptr,
+            a.j_dyn2 ? a.j_dyn2 + jd * 18 : nullptr, a.j_dyn3 ? a.j_dyn3 + jd * 36 : nullptr,
+            a.err_dyn ? a.err_dyn + jd : nullptr);
+    return;
+  }
+  const long jc = jd - nd;
+  if (jc < nd) {
+    const long t = jc / (a.L - 1), f = t * a.L + (jc - t * (a.L - 1));
+    cv_one(a.vel + f * 3, a.vel + (f + 1) * 3, a.isig_cv, a.r_cv + jc * 3, a.j_cv0 ? a.j_cv0 + jc * 9 : nullptr,
+           a.j_cv1 ? a.j_cv1 + jc * 9 : nullptr, a.err_cv ? a.err_cv + jc : nullptr);
   }
 }
 
@@ -488,6 +552,19 @@ int pa_cv_linearize(int n, const double* v1, const double* v2, const double* inv
   PA_CHECK(v1 && v2 && r, "null pointer");
   hipLaunchKernelGGL(pa::cv_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, n, v1, v2, inv_sigma, r,
                      j0, j1, err);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+int pa_trajectory_linearize(const pa_traj_args* a, void* stream) {
+  PA_CHECK(a, "null args");
+  PA_CHECK(a->T >= 0 && a->L >= 1 && a->n_kp >= 1, "T=%d L=%d n_kp=%d", a->T, a->L, a->n_kp);
+  if (a->T == 0) return PA_OK;
+  PA_CHECK(a->y && a->pose && a->vel && a->angvel && a->corners && a->K, "null input pointer");
+  PA_CHECK(a->r_proj && (a->L == 1 || (a->r_dyn && a->r_cv)), "null output pointer");
+  PA_CHECK(a->vel_frame == PA_VEL_WORLD || a->vel_frame == PA_VEL_BODY, "vel_frame must be 'world' or 'body'.");
+  const long n = (long)a->T * a->L * a->n_kp + 2L * a->T * (a->L - 1);
+  hipLaunchKernelGGL(pa::traj_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, *a);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -1,0 +1,113 @@
+"""Config 3: keypoint forward + per-frame factor linearize, fused on the GPU.
+
+The reference chains these through the host: `KeypointCNN.forward` (models.py:34-40)
+-> `.cpu()` -> kornia `denormalize_pixel_coordinates` (validate.py:144-153) -> one
+GTSAM `KeypointProjectionFactor` per keypoint (factors.py:182-275) plus one
+`PoseDynamicsFactor` (factors.py:8-142) and one `ConstantVelocityFactor`
+(factors.py:145-171) per consecutive frame pair, each evaluated through a Python
+callback.  Here the detector output never leaves HBM: `pa_trajectory_linearize`
+reads it directly, denormalizes in-kernel and evaluates every factor of T
+trajectories x L frames in ONE launch on the detector's stream.
+
+Layout (all device, f64 unless noted):
+  y        (T*L, 2K) f32   detector output, frame f = t*L + l
+  poses    (T*L, 12)       body pose per frame (R row-major, t)
+  vels     (T*L, 3)        linear velocity in `vel_frame`
+  angvels  (T*L, 3)        body angular velocity
+  corners  (K, 3)          keypoints in the body frame
+Outputs (factor order: projection f*K + k; dynamics / const-vel t*(L-1) + l):
+  proj: r (n,2), J (n,2,6), err (n,), status (n,) int32 (1 = cheirality)
+  dyn:  r (m,6), J0 (m,6,6), J1 (m,6,3), J2 (m,6,3), J3 (m,6,6), err (m,)
+  cv:   r (m,3), J0 (m,3,3), J1 (m,3,3), err (m,)
+Jacobians are whitened (A = H / sigma) and residuals r / sigma when sigmas are given,
+matching GTSAM's JacobianFactor (b = -r).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _f64(a, dev, shape=None):
+    if a is None:
+        return None
+    t = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a, np.float64))
+    t = t.to(device=dev, dtype=torch.float64).contiguous()
+    if shape is not None:
+        t = t.reshape(shape)
+    return t
+
+
+def _isig(sigmas, dim, dev):
+    if sigmas is None:
+        return None
+    s = np.broadcast_to(np.asarray(sigmas, np.float64).reshape(-1), (dim,))
+    return torch.as_tensor(1.0 / s, device=dev).contiguous()
+
+
+def linearize_trajectories(y: torch.Tensor, poses, vels, angvels, corners, K, *, T: int, L: int, dt: float,
+                           vel_frame: str = "world", camera_pose=None, H: int = 256, W: int = 256,
+                           proj_sigmas=None, dyn_sigmas=None, cv_sigmas=None, jacobians: bool = True) -> dict:
+    """All factors of T trajectories x L frames from the detector output `y` (device)."""
+    if y.device.type != "cuda":
+        raise RuntimeError("linearize_trajectories expects the detector output on the GPU (no CPU fallback)")
+    if vel_frame not in ("world", "body"):
+        raise AssertionError("vel_frame must be 'world' or 'body'.")  # factors.py:41
+    dev = y.device
+    F = T * L
+    y = y.to(torch.float32).contiguous()
+    if y.dim() != 2 or y.shape[0] != F or y.shape[1] % 2:
+        raise ValueError(f"y must be (T*L, 2K) = ({F}, 2K), got {tuple(y.shape)}")
+    nk = y.shape[1] // 2
+    P = _f64(poses, dev, (F, 12))
+    V = _f64(vels, dev, (F, 3))
+    Wv = _f64(angvels, dev, (F, 3))
+    Cn = _f64(corners, dev, (nk, 3))
+    Kt = _f64(K, dev, (5,))
+    Tc = _f64(camera_pose, dev, (12,))
+    isp, isd, isc = _isig(proj_sigmas, 2, dev), _isig(dyn_sigmas, 6, dev), _isig(cv_sigmas, 3, dev)
+    n, m = F * nk, T * max(L - 1, 0)
+
+    def e(*shape, dtype=torch.float64):
+        return torch.empty(shape, dtype=dtype, device=dev)
+
+    out = {"r_proj": e(n, 2), "status": e(n, dtype=torch.int32), "err_proj": e(n) if isp is not None else None,
+           "r_dyn": e(m, 6), "err_dyn": e(m) if isd is not None else None,
+           "r_cv": e(m, 3), "err_cv": e(m) if isc is not None else None}
+    # column-major per factor: allocate (n, cols, rows) and hand back the transpose
+    jac = {"j_proj": (n, 6, 2), "j_dyn0": (m, 6, 6), "j_dyn1": (m, 3, 6), "j_dyn2": (m, 3, 6),
+           "j_dyn3": (m, 6, 6), "j_cv0": (m, 3, 3), "j_cv1": (m, 3, 3)}
+    for k, shp in jac.items():
+        out[k] = e(*shp) if jacobians else None
+
+    a = _lib.TrajArgs()
+    a.T, a.L, a.n_kp, a.H, a.W = T, L, nk, H, W
+    a.y, a.pose, a.vel, a.angvel, a.corners, a.K = (t.data_ptr() for t in (y, P, V, Wv, Cn, Kt))
+    a.tcam = _lib.ptr(Tc)
+    a.dt = float(dt)
+    a.vel_frame = _lib.VEL_WORLD if vel_frame == "world" else _lib.VEL_BODY
+    a.isig_proj, a.isig_dyn, a.isig_cv = _lib.ptr(isp), _lib.ptr(isd), _lib.ptr(isc)
+    for k in ("r_proj", "err_proj", "status", "r_dyn", "err_dyn", "r_cv", "err_cv", *jac):
+        setattr(a, k, _lib.ptr(out[k]))
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pa_trajectory_linearize(C.byref(a), _lib.stream_of(dev)), "pa_trajectory_linearize")
+    for k in jac:
+        if out[k] is not None:
+            out[k] = out[k].transpose(1, 2)
+    out["_keep"] = (y, P, V, Wv, Cn, Kt, Tc, isp, isd, isc)  # inputs stay alive until the stream drains
+    return out
+
+
+def detect_and_linearize(model, x: torch.Tensor, poses, vels, angvels, corners, K, *, T: int, L: int, dt: float,
+                         **kw) -> dict:
+    """Config 3 end to end: `model(x)` then `linearize_trajectories` on the same stream;
+    the keypoints stay in HBM between the two launches."""
+    y = model(x)
+    out = linearize_trajectories(y, poses, vels, angvels, corners, K, T=T, L=L, dt=dt, H=model.H, W=model.W, **kw)
+    out["y"] = y
+    return out

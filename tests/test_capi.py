@@ -57,3 +57,27 @@ def test_bad_arguments_fail_loudly_without_touching_the_gpu():
 def test_gfx950_code_object_present():
     data = open(build.LIB, "rb").read()
     assert b"gfx950" in data
+
+
+def test_traj_args_struct_layout_matches_header(tmp_path):
+    """The ctypes mirror of pa_traj_args has the C compiler's field offsets."""
+    names = [f[0] for f in _lib.TrajArgs._fields_]
+    src = tmp_path / "off.c"
+    body = "".join(f'  printf("%zu\\n", offsetof(pa_traj_args, {n}));\n' for n in names)
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "perseus_amd.h"\nint main(void){\n'
+                   + body + '  printf("%zu\\n", sizeof(pa_traj_args));\n  return 0;\n}\n')
+    exe = tmp_path / "off"
+    import subprocess
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    want = [getattr(_lib.TrajArgs, n).offset for n in names] + [ctypes.sizeof(_lib.TrajArgs)]
+    assert got == want
+
+
+def test_trajectory_rejects_bad_shapes_without_gpu():
+    L = _lib.lib()
+    a = _lib.TrajArgs()
+    a.T, a.L, a.n_kp = 1, 0, 8
+    assert L.pa_trajectory_linearize(ctypes.byref(a), None) == -1
+    assert b"L=0" in L.pa_last_error()
+    assert L.pa_trajectory_linearize(None, None) == -1
