@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 MFMA_FP16_DENSE_PEAK = 2.5e15  # MI355X_MICROARCH.md: ~2.5 PF dense fp16/bf16
 MFMA_FP32_PEAK = 157.3e12      # f32-input MFMA peak (= vector f32 rate)
 HBM_PEAK = 8.0e12
+REPS = 20  # back-to-back launches per timed launch in the per-kernel pass
 
 
 def parse():
@@ -36,7 +37,7 @@ def parse():
     p.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--profile-passes", type=int, default=5)
+    p.add_argument("--profile-passes", type=int, default=3)
     return p.parse_args()
 
 
@@ -46,7 +47,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from perseus_amd import synth
+    from perseus_amd import shard, synth
     from perseus_amd.detector import KeypointCNN
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -80,9 +81,8 @@ def main():
         t0 = time.perf_counter()
         for i in range(args.steps):
             kp[i] = model(x)
-        if world > 1:  # one all-gather of all keypoints (configs[2])
-            gathered = [torch.empty_like(kp) for _ in range(world)]
-            dist.all_gather(gathered, kp)
+        if world > 1:  # one RCCL all-gather of every rank's keypoints (configs[2])
+            shard.gather_keypoints(kp.view(-1, kp.shape[-1]))
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -97,13 +97,14 @@ def main():
     value = frames / elapsed
     flops_frame = model.flops_per_frame()
 
-    # per-kernel HIP-event timing of the same forward on the same stream
-    prof_acc = {}
-    for _ in range(args.profile_passes):
-        prof, _ = model.profile(x)
-        for idx, (name, ms) in enumerate(prof):
-            prof_acc.setdefault((idx, name), []).append(ms)
-    per_launch = [(idx, name, statistics.median(v)) for (idx, name), v in sorted(prof_acc.items())]
+    # per-launch device time on the forward's stream: each launch of the forward issued
+    # REPS times back to back between two HIP events (pa_detector_time_launch), median
+    # over passes; no per-launch event gaps, so it agrees with rocprofv3 kernel-trace.
+    n_launch = len(model.profile(x)[0])
+    per_launch = []
+    for idx in range(n_launch):
+        v = [model.time_launch(x, idx, REPS) for _ in range(args.profile_passes)]
+        per_launch.append((idx, v[0][0], statistics.median(ms for _, ms in v)))
 
     line = None
     if rank == 0:
@@ -179,20 +180,14 @@ def roofline(per_launch, B, precision):
         return None
     groups = {}
     for (idx, name, ms), f in zip(per_launch, fl):
-        g = groups.setdefault(name, [0.0, 0.0, 0])
+        g = groups.setdefault(name, [0.0, 0.0, 0, []])
         g[0] += ms
         g[1] += f
         g[2] += 1
-    name, (ms, f, n) = max(groups.items(), key=lambda kv: kv[1][0])
+        g[3].append(idx)
+    name, (ms, f, n, idxs) = max(groups.items(), key=lambda kv: kv[1][0])
     peak = MFMA_FP16_DENSE_PEAK if precision == "fp16" else MFMA_FP32_PEAK
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            with open(tf) as fh:
-                traffic = json.load(fh).get(precision, {}).get(name)
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic(precision, B, idxs, [nm for _, nm, _ in per_launch])
     if f == 0:  # bandwidth kernel dominant (maxpool)
         return {"kernel": name, "bound": "hbm", "achieved": None, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": None, "traffic": traffic, "launches": n, "avg_ms": ms / n}
@@ -200,6 +195,23 @@ def roofline(per_launch, B, precision):
     return {"kernel": name, "bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": peak / 1e12,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic, "launches": n,
             "avg_ms": round(ms / n, 5), "flops_per_launch": f / n}
+
+
+def pmc_traffic(precision, B, idxs, names):
+    """Mean HBM bytes per launch of launch indices `idxs`, from the committed PMC
+    summary (profiles/pmc_traffic.json, tools/rocprof_summary.py: FETCH_SIZE x2 +
+    WRITE_SIZE, separate rocprofv3 --pmc passes), if it was taken on the same kernel
+    sequence and batch; else None."""
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(tf) as fh:
+            rec = json.load(fh).get(precision)
+    except (OSError, ValueError):
+        return None
+    if not rec or rec.get("batch") != B or rec.get("names") != names:
+        return None
+    v = [rec["bytes_per_launch"][i] for i in idxs]
+    return round(sum(v) / len(v))
 
 
 def px_error(model, x_host, state, dev, nframes=8):

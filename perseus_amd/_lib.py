@@ -48,6 +48,8 @@ _SIGS = {
     "pa_detector_profile": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_int]),
     "pa_detector_flops_per_frame": (C.c_double, [C.c_void_p]),
+    "pa_detector_time_launch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                          C.c_int, C.c_void_p, C.c_void_p]),
     "pa_debug_set_variant": (C.c_int, [C.c_int, C.c_int]),
     "pa_preprocess_rgbd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.c_float, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),

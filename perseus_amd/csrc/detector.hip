@@ -179,18 +179,52 @@ static int ensure_ws(pa_detector* d, int B) {
   return PA_OK;
 }
 
+// Per-launch device timing.  Mode 1 (target < 0): an event after every launch.
+// Mode 2 (target = launch index): that launch is issued `reps` times back to back
+// between two events and nothing else is marked, so the average is free of the
+// inter-kernel event overhead (~5 us per launch in mode 1).
 struct Prof {
   std::vector<hipEvent_t> ev;
   std::vector<const char*> names;
   hipStream_t s;
-  void mark(const char* name) {
+  int target = -1, reps = 1, cur = 0;
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  const char* target_name = nullptr;
+  void record(const char* name) {
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return;
     hipEventRecord(e, s);
     ev.push_back(e);
     names.push_back(name);
   }
+  void mark(const char* name) {
+    if (target < 0) record(name);
+  }
+  int count() const { return (target == cur) ? reps : 1; }
+  void before() {
+    if (target == cur) hipEventRecord(t0, s);
+  }
+  void after(const char* name) {
+    if (target == cur) {
+      hipEventRecord(t1, s);
+      target_name = name;
+    }
+    ++cur;
+    mark(name);
+  }
 };
+
+// one timed launch site: runs `call` once (or `reps` times if it is the profiled target)
+#define PA_RUN(call, name)                                \
+  do {                                                    \
+    const int _n = prof ? prof->count() : 1;              \
+    if (prof) prof->before();                             \
+    for (int _r = 0; _r < _n; ++_r) {                     \
+      int _rc = (call);                                   \
+      if (_rc != PA_OK) return _rc;                       \
+    }                                                     \
+    if (prof) prof->after(name);                          \
+  } while (0)
 
 #define PA_TRY(x)                \
   do {                           \
@@ -211,13 +245,10 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   const ConvL& st = d->convs[0];
   if constexpr (std::is_same<T, _Float16>::value) {
     // fused conv7x7 + BN + ReLU + maxpool: the 128x128 map stays on chip
-    PA_TRY(launch_stem_pool_fp16(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, X, s));
-    if (prof) prof->mark("stem_conv7x7_pool");
+    PA_RUN(launch_stem_pool_fp16(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, X, s), "stem_conv7x7_pool");
   } else {
-    PA_TRY(launch_stem<T>(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, S, s));
-    if (prof) prof->mark("stem_conv7x7");
-    PA_TRY(launch_maxpool<T>(S, B, 128, 128, 64, X, s));
-    if (prof) prof->mark("maxpool");
+    PA_RUN(launch_stem<T>(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, S, s), "stem_conv7x7");
+    PA_RUN(launch_maxpool<T>(S, B, 128, 128, 64, X, s), "maxpool");
   }
   int hw = 64;
   for (const Block& b : d->blocks) {
@@ -252,8 +283,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       sa.Hout = ho;
       sa.Wout = ho;
       sa.Cout = c1.cout;
-      PA_TRY(launch_conv3x3s2_ds<T>(sa, s, &kn));
-      if (prof) prof->mark(kn);
+      PA_RUN(launch_conv3x3s2_ds<T>(sa, s, &kn), kn);
       res = D;
       out = D;
     } else {
@@ -269,10 +299,9 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       a.pad = 1;
       a.epi = EPI_RELU;
       if (c1.stride == 1)
-        PA_TRY(launch_conv3x3_s1<T>(a, s, &kn));
+        PA_RUN(launch_conv3x3_s1<T>(a, s, &kn), kn);
       else
-        PA_TRY(launch_conv<T>(a, 3, s, &kn));
-      if (prof) prof->mark(kn);
+        PA_RUN(launch_conv<T>(a, 3, s, &kn), kn);
       if (b.ds >= 0) {
         const ConvL& cd = d->convs[b.ds];
         ConvArgs dsa = a;
@@ -281,8 +310,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
         dsa.out = D;
         dsa.pad = 0;
         dsa.epi = 0;
-        PA_TRY(launch_conv<T>(dsa, 1, s, &kn));
-        if (prof) prof->mark(kn);
+        PA_RUN(launch_conv<T>(dsa, 1, s, &kn), kn);
         res = D;
         out = D;
       }
@@ -305,13 +333,11 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     b2.stride = 1;
     b2.pad = 1;
     b2.epi = EPI_RELU | EPI_RES;
-    PA_TRY(launch_conv3x3_s1<T>(b2, s, &kn));
-    if (prof) prof->mark(kn);
+    PA_RUN(launch_conv3x3_s1<T>(b2, s, &kn), kn);
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
   }
-  PA_TRY(launch_head<T>(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s));
-  if (prof) prof->mark("avgpool_fc");
+  PA_RUN(launch_head<T>(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s), "avgpool_fc");
   return PA_OK;
 }
 
@@ -416,6 +442,37 @@ int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev,
   }
   for (hipEvent_t e : p.ev) hipEventDestroy(e);
   return rc == PA_OK ? n : rc;
+}
+
+int pa_detector_time_launch(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream, int index,
+                            int reps, float* avg_ms_out, const char** name_out) {
+  PA_CHECK(index >= 0 && reps >= 1, "index %d reps %d", index, reps);
+  pa::Prof p;
+  p.s = (hipStream_t)stream;
+  p.target = index;
+  p.reps = reps;
+  if (hipEventCreate(&p.t0) != hipSuccess || hipEventCreate(&p.t1) != hipSuccess) {
+    pa::set_error("time_launch: hipEventCreate failed");
+    return PA_EHIP;
+  }
+  int rc = pa::forward(d, x_dev, B, y_dev, p.s, &p);
+  if (rc == PA_OK && !p.target_name) {
+    pa::set_error("time_launch: launch index %d out of range (%d launches)", index, p.cur);
+    rc = PA_EINVAL;
+  }
+  if (rc == PA_OK && hipStreamSynchronize(p.s) != hipSuccess) {
+    pa::set_error("time_launch: stream sync failed");
+    rc = PA_EHIP;
+  }
+  if (rc == PA_OK) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, p.t0, p.t1);
+    if (avg_ms_out) *avg_ms_out = ms / reps;
+    if (name_out) *name_out = p.target_name;
+  }
+  hipEventDestroy(p.t0);
+  hipEventDestroy(p.t1);
+  return rc;
 }
 
 int pa_debug_set_variant(int layer, int variant) {

@@ -192,6 +192,25 @@ class KeypointCNN(nn.Module):
         return [(names[i].decode(), ms[i]) for i in range(n)], y
 
 
+    def time_launch(self, x: torch.Tensor, index: int, reps: int = 20):
+        """(name, avg ms) of launch `index` of the forward, issued `reps` times back to
+        back between two HIP events on the current stream (no per-launch event gaps)."""
+        x, _ = self._prep(x)
+        dev = x.device
+        h = self._ensure_handle(dev)
+        L = _lib.lib()
+        _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP32 if self.precision == "fp32" else _lib.PREC_FP16),
+                   "set_precision")
+        y = torch.empty((x.shape[0], 2 * self.n_keypoints), dtype=torch.float32, device=dev)
+        ms = _lib.C.c_float()
+        name = _lib.C.c_char_p()
+        with torch.cuda.device(dev):
+            _lib.check(L.pa_detector_time_launch(h, x.data_ptr(), x.shape[0], y.data_ptr(), _lib.stream_of(dev),
+                                                 index, reps, _lib.C.byref(ms), _lib.C.byref(name)),
+                       "pa_detector_time_launch")
+        return name.value.decode(), ms.value
+
+
 def denormalize_pixel_coordinates(y: torch.Tensor, H: int = 256, W: int = 256, target: torch.Tensor | None = None):
     """Device post-processing (validate.py:130-153): normalized (B,2K) -> px (B,K,2),
     plus SmoothL1(beta=1, reduction='none') against normalized targets if given."""
