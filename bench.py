@@ -38,6 +38,7 @@ def parse():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-passes", type=int, default=3)
+    p.add_argument("--no-factors", action="store_true")
     return p.parse_args()
 
 
@@ -106,6 +107,8 @@ def main():
         v = [model.time_launch(x, idx, REPS) for _ in range(args.profile_passes)]
         per_launch.append((idx, v[0][0], statistics.median(ms for _, ms in v)))
 
+    fac = factor_leg(dev, args.seed, rank) if not args.no_factors else None
+
     line = None
     if rank == 0:
         roof = roofline(per_launch, B, args.precision)
@@ -135,6 +138,7 @@ def main():
             "px_l2": px,
             "cpu_baseline": cpu,
             "kernels_ms": {f"{i:02d}_{n}": round(ms, 4) for i, n, ms in per_launch},
+            "factors": fac,
         }
         print(json.dumps(line))
     if world > 1:
@@ -195,6 +199,40 @@ def roofline(per_launch, B, precision):
     return {"kernel": name, "bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": peak / 1e12,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic, "launches": n,
             "avg_ms": round(ms / n, 5), "flops_per_launch": f / n}
+
+
+def factor_leg(dev, seed, rank, T=1000, L=24, reps=20):
+    """Config 3 side measurement: pa_trajectory_linearize over 1000 trajectories x 24
+    frames (8 projection factors per frame, a dynamics + const-vel factor per frame
+    pair, whitened, Jacobians on), `reps` launches back to back between HIP events on
+    the launch stream.  Algorithmic bytes: every input read once, every output written
+    once (DESIGN.md "factor kernels")."""
+    import torch
+
+    from perseus_amd import pipeline, synth
+
+    tr = synth.synthetic_trajectories(seed + 1 + rank, T, L)
+    y = torch.as_tensor(tr["y"], device=dev)
+    a, out = pipeline.prepare_trajectories(y, tr["poses"], tr["vels"], tr["angvels"], tr["corners"], tr["K"], T=T,
+                                           L=L, dt=1 / 12, proj_sigmas=[1.0, 1.0], dyn_sigmas=[0.1] * 6,
+                                           cv_sigmas=[0.1] * 3)
+    for _ in range(3):
+        pipeline.launch(a, dev)
+    s = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        pipeline.launch(a, dev)
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    F, n, m = T * L, T * L * 8, T * (L - 1)
+    bytes_in = F * (16 * 4 + 12 * 8 + 3 * 8 + 3 * 8)
+    bytes_out = n * (2 + 12 + 1) * 8 + n * 4 + m * (6 + 36 + 18 + 18 + 36 + 1) * 8 + m * (3 + 9 + 9 + 1) * 8
+    return {"workload": f"trajectory_linearize_{T}x{L}", "frames": F, "factors": n + 2 * m,
+            "us_per_launch": round(t * 1e6, 2), "frames_per_s": round(F / t, 1), "factors_per_s": round((n + 2 * m) / t),
+            "alg_bytes": bytes_in + bytes_out, "hbm_gbps": round((bytes_in + bytes_out) / t / 1e9, 1),
+            "hbm_frac": round((bytes_in + bytes_out) / t / HBM_PEAK, 4), "dtype": "f64"}
 
 
 def pmc_traffic(precision, B, idxs, names):

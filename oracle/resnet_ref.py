@@ -92,6 +92,18 @@ def denormalize(y: np.ndarray, H: int = 256, W: int = 256) -> np.ndarray:
     return (y + 1.0) * scale
 
 
+def denormalize_f32(y: np.ndarray, H: int = 256, W: int = 256) -> np.ndarray:
+    """kornia.geometry.conversions.denormalize_pixel_coordinates (kornia, unpinned
+    version: absent here) operation for operation in f32, as validate.py:144-153 and
+    streaming.py:129-131 run it on f32 model outputs:
+        hw = stack([W, H]); factor = 2 / (hw - 1).clamp(eps); px = 1 / factor * (n + 1)
+    (1 / f32(2/255) = 127.49999237, so this differs from 127.5 (n+1) by <= 1.6e-5 px)."""
+    y = np.asarray(y, dtype=np.float32).reshape(np.shape(y)[0], -1, 2)
+    hw = np.array([W, H], np.float32)
+    factor = np.float32(2.0) / np.maximum(hw - np.float32(1), np.float32(1e-8))
+    return (np.float32(1.0) / factor) * (y + np.float32(1.0))
+
+
 # --------------------------------------------------------------------------------------
 # torchvision.models stand-in (module tree with torchvision's names; no weight download).
 # Used ONLY by oracle/gen_golden.py to import the reference's KeypointCNN here.

@@ -41,4 +41,12 @@ void set_error(const char* fmt, ...);
     }                                                                                  \
   } while (0)
 
+// kornia.geometry.conversions.denormalize_pixel_coordinates in f32, operation for
+// operation: factor = 2 / (S - 1); px = (1 / factor) * (n + 1).  (1 / f32(2/255) is
+// 127.49999237, not 127.5: the reference's pixels carry that rounding.)
+__host__ __device__ __forceinline__ float kornia_denorm(float n, int S) {
+  const float factor = 2.0f / (float)(S - 1);
+  return (1.0f / factor) * (n + 1.0f);
+}
+
 }  // namespace pa

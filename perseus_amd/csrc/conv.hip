@@ -568,15 +568,15 @@ int launch_preprocess(const uint8_t* rgb, const float* depth, int B, int Hs, int
   return PA_OK;
 }
 
-// kornia denormalize_pixel_coordinates (validate.py:144-153) + SmoothL1(beta=1,
+// kornia denormalize_pixel_coordinates (validate.py:144-153; kornia_denorm in
+// common.h) + SmoothL1(beta=1,
 // reduction='none') against normalized targets (validate.py:130-133).
 __global__ void postprocess_kernel(const float* __restrict__ y, const float* __restrict__ target, int total, int H,
                                    int W, float* __restrict__ px, float* __restrict__ loss) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const float v = y[i];
-  const float f = (i & 1) ? (float)(H - 1) / 2.0f : (float)(W - 1) / 2.0f;
-  px[i] = (v + 1.0f) * f;
+  px[i] = kornia_denorm(v, (i & 1) ? H : W);
   if (target) {
     const float d = fabsf(target[i] - v);
     loss[i] = d < 1.0f ? 0.5f * d * d : d - 0.5f;

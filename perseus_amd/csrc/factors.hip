@@ -494,7 +494,7 @@ __global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restric
 
 // Config 3: all factors of T trajectories x L frames in one launch, measurements
 // straight from the detector output y (normalized, denormalized here exactly as
-// kornia's denormalize_pixel_coordinates: px = (n + 1) (S - 1) / 2 in f32).
+// kornia's denormalize_pixel_coordinates in f32, common.h kornia_denorm).
 // Thread index space: [proj: T*L*K | dyn: T*(L-1) | cv: T*(L-1)].
 __global__ __launch_bounds__(64) void traj_kernel(pa_traj_args a) {
   const long i = blockIdx.x * 64L + threadIdx.x;
@@ -504,8 +504,8 @@ __global__ __launch_bounds__(64) void traj_kernel(pa_traj_args a) {
     const long f = i / a.n_kp;
     const int k = (int)(i - f * a.n_kp);
     const float* yf = a.y + f * 2 * a.n_kp + 2 * k;
-    const float px = (yf[0] + 1.0f) * ((float)(a.W - 1) / 2.0f);
-    const float py = (yf[1] + 1.0f) * ((float)(a.H - 1) / 2.0f);
+    const float px = kornia_denorm(yf[0], a.W);
+    const float py = kornia_denorm(yf[1], a.H);
     proj_one(a.pose + f * 12, load3(a.corners + 3 * k), (double)px, (double)py, a.K, a.tcam, a.isig_proj,
              a.r_proj + i * 2, a.j_proj ? a.j_proj + i * 12 : nullptr, a.err_proj ? a.err_proj + i : nullptr,
              a.status ? a.status + i : nullptr);

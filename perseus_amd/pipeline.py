@@ -50,10 +50,13 @@ def _isig(sigmas, dim, dev):
     return torch.as_tensor(1.0 / s, device=dev).contiguous()
 
 
-def linearize_trajectories(y: torch.Tensor, poses, vels, angvels, corners, K, *, T: int, L: int, dt: float,
-                           vel_frame: str = "world", camera_pose=None, H: int = 256, W: int = 256,
-                           proj_sigmas=None, dyn_sigmas=None, cv_sigmas=None, jacobians: bool = True) -> dict:
-    """All factors of T trajectories x L frames from the detector output `y` (device)."""
+def prepare_trajectories(y: torch.Tensor, poses, vels, angvels, corners, K, *, T: int, L: int, dt: float,
+                         vel_frame: str = "world", camera_pose=None, H: int = 256, W: int = 256,
+                         proj_sigmas=None, dyn_sigmas=None, cv_sigmas=None, jacobians: bool = True):
+    """Stage inputs on the device and allocate outputs: returns (args, out).  `args`
+    (a pa_traj_args) can be launched repeatedly with `launch(args, device)`; `out`
+    holds the output tensors (Jacobians as (n, cols, rows) column-major buffers) and
+    keeps every staged input alive."""
     if y.device.type != "cuda":
         raise RuntimeError("linearize_trajectories expects the detector output on the GPU (no CPU fallback)")
     if vel_frame not in ("world", "body"):
@@ -79,11 +82,8 @@ def linearize_trajectories(y: torch.Tensor, poses, vels, angvels, corners, K, *,
     out = {"r_proj": e(n, 2), "status": e(n, dtype=torch.int32), "err_proj": e(n) if isp is not None else None,
            "r_dyn": e(m, 6), "err_dyn": e(m) if isd is not None else None,
            "r_cv": e(m, 3), "err_cv": e(m) if isc is not None else None}
-    # column-major per factor: allocate (n, cols, rows) and hand back the transpose
-    jac = {"j_proj": (n, 6, 2), "j_dyn0": (m, 6, 6), "j_dyn1": (m, 3, 6), "j_dyn2": (m, 3, 6),
-           "j_dyn3": (m, 6, 6), "j_cv0": (m, 3, 3), "j_cv1": (m, 3, 3)}
-    for k, shp in jac.items():
-        out[k] = e(*shp) if jacobians else None
+    for k, shp in _JAC.items():
+        out[k] = e(*((n, m)[shp[0]],) + shp[1:]) if jacobians else None
 
     a = _lib.TrajArgs()
     a.T, a.L, a.n_kp, a.H, a.W = T, L, nk, H, W
@@ -92,14 +92,33 @@ def linearize_trajectories(y: torch.Tensor, poses, vels, angvels, corners, K, *,
     a.dt = float(dt)
     a.vel_frame = _lib.VEL_WORLD if vel_frame == "world" else _lib.VEL_BODY
     a.isig_proj, a.isig_dyn, a.isig_cv = _lib.ptr(isp), _lib.ptr(isd), _lib.ptr(isc)
-    for k in ("r_proj", "err_proj", "status", "r_dyn", "err_dyn", "r_cv", "err_cv", *jac):
+    for k in ("r_proj", "err_proj", "status", "r_dyn", "err_dyn", "r_cv", "err_cv", *_JAC):
         setattr(a, k, _lib.ptr(out[k]))
-    with torch.cuda.device(dev):
-        _lib.check(_lib.lib().pa_trajectory_linearize(C.byref(a), _lib.stream_of(dev)), "pa_trajectory_linearize")
-    for k in jac:
+    out["_keep"] = (y, P, V, Wv, Cn, Kt, Tc, isp, isd, isc)  # inputs stay alive until the stream drains
+    return a, out
+
+
+# column-major per factor: (0 = proj rows / 1 = dyn,cv rows, cols, rows)
+_JAC = {"j_proj": (0, 6, 2), "j_dyn0": (1, 6, 6), "j_dyn1": (1, 3, 6), "j_dyn2": (1, 3, 6), "j_dyn3": (1, 6, 6),
+        "j_cv0": (1, 3, 3), "j_cv1": (1, 3, 3)}
+
+
+def launch(args, device) -> None:
+    """One pa_trajectory_linearize launch on `device`'s current stream."""
+    with torch.cuda.device(device):
+        _lib.check(_lib.lib().pa_trajectory_linearize(C.byref(args), _lib.stream_of(device)),
+                   "pa_trajectory_linearize")
+
+
+def linearize_trajectories(y: torch.Tensor, poses, vels, angvels, corners, K, *, T: int, L: int, dt: float,
+                           **kw) -> dict:
+    """All factors of T trajectories x L frames from the detector output `y` (device).
+    Keywords as `prepare_trajectories`; Jacobians are returned as (n, rows, cols) views."""
+    a, out = prepare_trajectories(y, poses, vels, angvels, corners, K, T=T, L=L, dt=dt, **kw)
+    launch(a, y.device)
+    for k in _JAC:
         if out[k] is not None:
             out[k] = out[k].transpose(1, 2)
-    out["_keep"] = (y, P, V, Wv, Cn, Kt, Tc, isp, isd, isc)  # inputs stay alive until the stream drains
     return out
 
 

@@ -37,6 +37,7 @@ FC_SCALE = 0.2
 STREAM_RGB = 1 << 20
 STREAM_DEPTH = (1 << 20) + 1
 STREAM_DEPTH_MASK = (1 << 20) + 2
+STREAM_TRAJ = (1 << 20) + 3
 
 DEPTH_SCALE = 0.035  # augmentations.py:263 cube_scale; streaming.py:76 `/= 0.035`
 
@@ -173,6 +174,32 @@ def synthetic_frames(seed: int, batch: int, in_ch: int = 4, H: int = 256, W: int
             d[u2 < 0.25] = 0.0
             out[b, 3] = d.astype(np.float32).reshape(H, W)
     return out
+
+
+CUBE_CORNERS = np.array([[x, y, z] for x in (-1, 1) for y in (-1, 1) for z in (-1, 1)], np.float64) * 0.0175
+CAMERA_K = np.array([280.0, 280.0, 0.0, 128.0, 128.0])  # Cal3_S2 of the datagen camera
+
+
+def synthetic_trajectories(seed: int, T: int, L: int, n_kp: int = 8) -> dict:
+    """T trajectories x L frames of smoother inputs:
+    poses (T*L, 12) with R = Exp(U(-.5,.5)^3) and t = (U(+-.05), U(+-.05), U(.3,.5)) in
+    front of the identity camera; vels / angvels U(-1,1)^3; detector-like normalized
+    keypoints y U(-1,1) (T*L, 2K) f32."""
+    F = T * L
+    u = uniform(seed, STREAM_TRAJ, F * (3 + 3 + 3 + 3) + F * 2 * n_kp).astype(np.float64)
+    w = (u[:3 * F].reshape(F, 3) - 0.5)
+    t = u[3 * F:6 * F].reshape(F, 3)
+    t = np.stack([0.1 * t[:, 0] - 0.05, 0.1 * t[:, 1] - 0.05, 0.3 + 0.2 * t[:, 2]], 1)
+    vel = 2 * u[6 * F:9 * F].reshape(F, 3) - 1
+    ang = 2 * u[9 * F:12 * F].reshape(F, 3) - 1
+    y = (2 * u[12 * F:].reshape(F, 2 * n_kp) - 1).astype(np.float32)
+    th = np.linalg.norm(w, axis=1)[:, None, None]
+    Wx = np.zeros((F, 3, 3))
+    Wx[:, 0, 1], Wx[:, 0, 2], Wx[:, 1, 2] = -w[:, 2], w[:, 1], -w[:, 0]
+    Wx = Wx - Wx.transpose(0, 2, 1)
+    R = np.eye(3) + np.sin(th) / th * Wx + (1 - np.cos(th)) / th ** 2 * (Wx @ Wx)
+    poses = np.concatenate([R.reshape(F, 9), t], 1)
+    return {"poses": poses, "vels": vel, "angvels": ang, "y": y, "corners": CUBE_CORNERS[:n_kp], "K": CAMERA_K}
 
 
 def sha256(a: np.ndarray) -> str:

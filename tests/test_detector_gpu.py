@@ -123,8 +123,11 @@ def test_postprocess_matches_validate_py():
     y = torch.rand(4, 16, device="cuda") * 2 - 1
     t = torch.rand(4, 16, device="cuda") * 2 - 1
     px, loss = denormalize_pixel_coordinates(y, 256, 256, target=t)
-    ref_px = ((y.reshape(4, 8, 2) + 1) * 127.5)
+    # kornia denormalize_pixel_coordinates, operation for operation (oracle.resnet_ref.denormalize_f32)
+    factor = torch.tensor(2.0) / (torch.tensor([256.0, 256.0]) - 1).clamp(1e-8)
+    ref_px = torch.tensor(1.0) / factor.cuda() * (y.reshape(4, 8, 2) + 1)
     assert torch.equal(px, ref_px)
+    np.testing.assert_array_equal(px.cpu().numpy(), R.denormalize_f32(y.cpu().numpy()))
     ref_loss = torch.nn.SmoothL1Loss(beta=1.0, reduction="none")(t, y)
     assert torch.allclose(loss, ref_loss, atol=0, rtol=0)
 

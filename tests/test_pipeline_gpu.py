@@ -5,6 +5,7 @@ import pytest
 import torch
 
 from oracle import factors_ref as F
+from oracle import resnet_ref as R
 from perseus_amd import pipeline
 
 pytestmark = pytest.mark.gpu
@@ -32,9 +33,7 @@ def _problem(T, L, seed, behind=()):
 
 def _denorm(y, H=256, W=256):
     """kornia denormalize_pixel_coordinates in f32 (validate.py:144-153)."""
-    px = y.reshape(y.shape[0], -1, 2).astype(np.float32)
-    f = np.array([np.float32(W - 1) / np.float32(2), np.float32(H - 1) / np.float32(2)], np.float32)
-    return ((px + np.float32(1)) * f).astype(np.float64)
+    return R.denormalize_f32(y, H, W).astype(np.float64)
 
 
 def _oracle(poses, vels, angvels, y, T, L, dt, vf, Tc=None):
@@ -124,3 +123,35 @@ def test_detect_and_linearize_uses_device_keypoints():
     y = out["y"].cpu().numpy()
     ref = _oracle(poses, vels, angvels, y, T, L, 1 / 12, "world")
     _cmp(out, ref)
+
+
+def test_full_size_config3_sampled_vs_oracle():
+    """BASELINE configs[3] size (1000 trajectories x 24 frames): a seeded sample of
+    every factor type against the oracle, plus properties over all of them."""
+    from perseus_amd import synth
+
+    T, L, dt = 1000, 24, 1 / 12
+    tr = synth.synthetic_trajectories(5, T, L)
+    out = pipeline.linearize_trajectories(torch.as_tensor(tr["y"], device="cuda"), tr["poses"], tr["vels"],
+                                          tr["angvels"], tr["corners"], tr["K"], T=T, L=L, dt=dt)
+    rng = np.random.default_rng(0)
+    nk = 8
+    z = _denorm(tr["y"]).reshape(-1, 2)
+    for i in rng.choice(T * L * nk, 300, replace=False):
+        f, k = divmod(int(i), nk)
+        r, H0, st, _ = F.projection(F.unpack(tr["poses"][f]), tr["corners"][k], z[i], tr["K"])
+        assert out["status"][i].item() == st == 0
+        np.testing.assert_allclose(out["r_proj"][i].cpu().numpy(), r, atol=ATOL, rtol=0)
+        np.testing.assert_allclose(out["j_proj"][i].cpu().numpy(), H0, atol=ATOL, rtol=1e-12)
+    for j in rng.choice(T * (L - 1), 100, replace=False):
+        t, l = divmod(int(j), L - 1)
+        f = t * L + l
+        r, H = F.dynamics(F.unpack(tr["poses"][f]), tr["angvels"][f], tr["vels"][f], F.unpack(tr["poses"][f + 1]),
+                          dt, "world")
+        np.testing.assert_allclose(out["r_dyn"][j].cpu().numpy(), r, atol=ATOL, rtol=0)
+        for q in range(4):
+            np.testing.assert_allclose(out[f"j_dyn{q}"][j].cpu().numpy(), H[q], atol=ATOL, rtol=1e-12)
+    # whole-array properties: every corner is in front of the camera; const-vel exact
+    assert int(out["status"].sum()) == 0 and torch.isfinite(out["j_proj"]).all()
+    v = torch.as_tensor(tr["vels"], device="cuda").reshape(T, L, 3)
+    assert torch.equal(out["r_cv"].reshape(T, L - 1, 3), v[:, 1:] - v[:, :-1])

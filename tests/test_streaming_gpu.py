@@ -1,0 +1,60 @@
+"""Config 4 pipeline: graph replay == eager composition, and matches the reference
+arithmetic of scripts/streaming.py:59-82 + 126-131 on the same frames."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import resnet_ref as R
+from perseus_amd import synth
+from perseus_amd.detector import KeypointCNN, preprocess_rgbd
+from perseus_amd.streaming import StreamingPipeline
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def model():
+    m = KeypointCNN(num_channels=4)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
+    return m
+
+
+def _frames(seed, n=3, Hs=720, Ws=1280):
+    rng = np.random.default_rng(seed)
+    rgb = rng.integers(0, 256, (n, Hs, Ws, 3), dtype=np.uint8)
+    d = rng.uniform(0.12, 0.48, (n, Hs, Ws)).astype(np.float32)
+    d[:, ::7, ::5] = np.nan
+    d[:, 3::11, ::3] = np.inf
+    return rgb, d
+
+
+@pytest.mark.parametrize("host_crop", [True, False])
+def test_graph_matches_eager(model, host_crop):
+    rgb, d = _frames(1)
+    g = StreamingPipeline(model, host_crop=host_crop, graph=True)
+    e = StreamingPipeline(model, host_crop=host_crop, graph=False)
+    for seed in (1, 2):
+        rgb, d = _frames(seed)
+        np.testing.assert_array_equal(g(rgb, d), e(rgb, d))
+
+
+def test_matches_reference_frame_arithmetic(model):
+    rgb, d = _frames(3)
+    out = StreamingPipeline(model)(rgb, d)
+    # streaming.py:68-80 in numpy, then crop, then the model
+    xs = []
+    for i in range(3):
+        fr = rgb[i][..., ::-1] / 255.0
+        dep = d[i].copy()
+        dep[np.isnan(dep)] = 0
+        dep[np.isinf(dep)] = 0
+        dep /= 0.035
+        fr = np.concatenate([fr, dep[..., None]], axis=-1)
+        H, W = fr.shape[:2]
+        fr = fr[H // 2 - 128:H // 2 + 128, W // 2 - 128:W // 2 + 128]
+        xs.append(torch.from_numpy(fr).permute(2, 0, 1).float())
+    x = torch.stack(xs).cuda()
+    x_dev = preprocess_rgbd(torch.as_tensor(rgb).cuda(), torch.as_tensor(d).cuda())
+    assert torch.equal(x, x_dev)
+    y = model(x).reshape(3, -1, 2)
+    np.testing.assert_array_equal(out, R.denormalize_f32(y.cpu().numpy().reshape(3, -1)))
