@@ -87,16 +87,15 @@ __device__ __forceinline__ int frag_off(int r) { return r < 4 ? 2 * r : (r < 12 
 template <int V>
 using ic = std::integral_constant<int, V>;
 
-template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int EPI, int SB, int TPS,
-          int WD, int ABL = 0>
-__global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
+template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int EPI, int TPW>
+__global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a, int ntiles) {
   constexpr int NT = WM * WN * 64;
   constexpr int KB = PElem<T>::KB;
   constexpr int CPR = 16 / sizeof(T);
   constexpr int NCB = CIN / KB;  // 128-byte channel blocks
-  constexpr int SPC = 9 / TPS;   // steps per channel block (TPS taps per step)
+  constexpr int SPC = 9;         // steps (filter taps) per channel block
   constexpr int NSTEPS = NCB * SPC;
-  static_assert(TPS == 1 || TPS == 3, "taps per step");
+  constexpr int WD = 3;          // weight register sets (prefetch distance)
   constexpr int KTOT = 9 * CIN;
   constexpr int PH = TH + 2, PW = TW + 2;
   // per-image patch stride in pixels; for 8-wide tiles a fragment pairs one row of
@@ -107,14 +106,13 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int PCH = (NP * 8 + NT - 1) / NT;  // patch 16-B chunks per thread
-  constexpr int BCH = TPS * BN * 8 / NT;       // weight chunks per thread
-  static_assert(TPS * BN * 8 % NT == 0, "weight tile / threads");
+  constexpr int BCH = BN * 8 / NT;             // weight chunks per thread
+  static_assert(BN * 8 % NT == 0, "weight tile / threads");
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
   static_assert(TW >= 16 || (TW == 8 && NI == 2), "fragment geometry");
-  static_assert(PBUF == 2 || NCB == 1 || true, "");
+  static_assert(SPC % WD == 0, "register-set rotation must be static");
   constexpr int PATCHB = NP * 128;
-  constexpr int WB1 = BN * 128;  // one tap's weight tile
-  constexpr int WB = TPS * WB1;
+  constexpr int WB = BN * 128;  // one tap's weight tile
   __shared__ __attribute__((aligned(16))) char smem[PBUF * PATCHB + 2 * WB];
   char* patch = smem;
   char* wbuf = smem + PBUF * PATCHB;
@@ -128,21 +126,27 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   const T* __restrict__ in = (const T*)a.in;
   const T* __restrict__ w = (const T*)a.w;
 
-  // tile decode: N-tiles of one spatial tile are adjacent (share the patch in L2)
+  // Tiles: N-tiles of one spatial tile are adjacent in the tile index (they share
+  // the patch in L2).  A workgroup takes tiles blockIdx.x + t * gridDim.x, t < TPW;
+  // gridDim.x is a multiple of the N-tile count, so its output channels (and the
+  // streamed weights) are the same for all its tiles, and the next tile's patch is
+  // prefetched while the current one computes.
   const int ntn = Cout / BN;
-  const int tn_idx = blockIdx.x % ntn;
-  const int sp = blockIdx.x / ntn;
+  const int n0 = (blockIdx.x % ntn) * BN;
   const int tw_n = W / TW, tpi = (H / TH) * tw_n;
-  const int img0 = (sp / tpi) * NI;
-  const int rem = sp - (sp / tpi) * tpi;
-  const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
-  const int n0 = tn_idx * BN;
+  struct Tile {
+    int img0, th0, tw0;
+  };
+  auto decode = [&](int tile) __attribute__((always_inline)) {
+    const int sp = tile / ntn;
+    const int rem = sp - (sp / tpi) * tpi;
+    return Tile{(sp / tpi) * NI, (rem / tw_n) * TH, (rem - (rem / tw_n) * tw_n) * TW};
+  };
 
   // ---- staging (register-staged; hipcc counts these loads itself)
   u32x4 rp[PCH];
-  static_assert(SPC % WD == 0, "register-set rotation must be static");
   u32x4 rb[WD][BCH];
-  auto load_patch = [&](int cb) __attribute__((always_inline)) {
+  auto load_patch = [&](const Tile& tl, int cb) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PCH; ++i) {
       const int c = tid + i * NT;
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
         const int p = c >> 3, ch = c & 7;
         const int img = p / IMS, pp = p - (p / IMS) * IMS;
         const int pr = pp / PW, pc = pp - (pp / PW) * PW;
-        const int n = img0 + img, h = th0 + pr - 1, x = tw0 + pc - 1;
+        const int n = tl.img0 + img, h = tl.th0 + pr - 1, x = tl.tw0 + pc - 1;
         if (pr < PH && n < a.B && (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W)
           v = *reinterpret_cast<const u32x4*>(in + (((size_t)n * H + h) * W + x) * Cin + cb * KB + ch * CPR);
       }
@@ -167,13 +171,11 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   };
   auto load_w = [&](int s, auto setc) __attribute__((always_inline)) {
     constexpr int SET = decltype(setc)::value;
-    const int cb = s / SPC, st = s - (s / SPC) * SPC;
+    const int cb = s / SPC, tap = s - (s / SPC) * SPC;
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * NT;
-      const int kc = c / (BN * 8), cc = c - (c / (BN * 8)) * (BN * 8);
-      const int row = cc >> 3, ch = cc & 7;
-      const int tap = st * TPS + kc;
+      const int row = c >> 3, ch = c & 7;
       rb[SET][i] = *reinterpret_cast<const u32x4*>(w + (size_t)(n0 + row) * KTOT + tap * Cin + cb * KB + ch * CPR);
     }
   };
@@ -182,12 +184,11 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int c = tid + i * NT;
-      const int kc = c / (BN * 8), cc = c - (c / (BN * 8)) * (BN * 8);
-      *reinterpret_cast<u32x4*>(wbuf + buf * WB + kc * WB1 + pswz(cc >> 3, cc & 7)) = rb[SET][i];
+      *reinterpret_cast<u32x4*>(wbuf + buf * WB + pswz(c >> 3, c & 7)) = rb[SET][i];
     }
   };
 
-  // per-lane patch pixel (tap (0,0)) of each pixel fragment
+  // per-lane patch pixel (tap (0,0)) of each pixel fragment (tile independent)
   const int o = frag_off(r16);
   int ppix[TM];
 #pragma unroll
@@ -204,102 +205,88 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
   }
 
   f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Tile cur = decode(blockIdx.x);
+  const int my_tiles = blockIdx.x + (TPW - 1) * (int)gridDim.x < ntiles
+                           ? TPW
+                           : (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
 
-  load_patch(0);
+  load_patch(cur, 0);
   load_w(0, ic<0>{});
   store_patch(0);
   store_w(0, ic<0>{});
   load_w(NSTEPS > 1 ? 1 : 0, ic<1>{});
-  load_w(NSTEPS > 2 ? 2 : 0, ic<2 % WD>{});
-  if constexpr (WD == 9) {
-    load_w(NSTEPS > 3 ? 3 : 0, ic<3 % WD>{});
-    load_w(NSTEPS > 4 ? 4 : 0, ic<4 % WD>{});
-    load_w(NSTEPS > 5 ? 5 : 0, ic<5 % WD>{});
-    load_w(NSTEPS > 6 ? 6 : 0, ic<6 % WD>{});
-    load_w(NSTEPS > 7 ? 7 : 0, ic<7 % WD>{});
-    load_w(NSTEPS > 8 ? 8 : 0, ic<8 % WD>{});
-  }
+  load_w(NSTEPS > 2 ? 2 : 0, ic<2>{});
   __syncthreads();
 
-  u32x4 fa0[2][TN], fb0[2][TM];  // ablation (ABL >= 2): fragments reused from step 0
-  // One K-step (cb, ST): TPS filter taps.  Refill register set ST%3 with W(s+3),
-  // MFMAs on the staged W(s) and patch(cb), then W(s+1) (set (ST+1)%3) -> the
-  // other LDS buffer.  Weight loads stay in flight for ~2 steps, the next block's
-  // patch for the whole channel block.  Every load/store is unconditional
-  // (indices are clamped) so that hipcc's vmcnt bookkeeping stays exact.
-  auto step = [&](int cb, auto stc) __attribute__((always_inline)) {
-    constexpr int ST = decltype(stc)::value;
-    const int s = cb * SPC + ST;
-    if constexpr (ABL == 0) load_w(s + WD < NSTEPS ? s + WD : NSTEPS - 1, ic<ST % WD>{});
-    if constexpr (ST == 0 && NCB > 1 && ABL == 0) load_patch(cb + 1 < NCB ? cb + 1 : NCB - 1);
-    const char* pb = patch + (PBUF == 2 ? (cb & 1) * PATCHB : 0);
-    const char* wb = wbuf + (s & 1) * WB;
+  // Weight-step index runs on across tiles (W(s) of tile t+1 = W(s) of tile t),
+  // so the prefetch distance WD wraps modulo NSTEPS; gs = global step for the LDS
+  // ring parity.
+  int gs = 0;
+  for (int t = 0; t < TPW; ++t) {
+    if (TPW > 1 && t >= my_tiles) break;
+    const bool more = TPW > 1 && t + 1 < my_tiles;
+    Tile nxt = cur;
+    if (more) nxt = decode(blockIdx.x + (t + 1) * (int)gridDim.x);
 #pragma unroll
-    for (int kc = 0; kc < TPS; ++kc) {
-      const int tap = ST * TPS + kc;
-      const int toff = (tap / 3) * PW + (tap % 3);
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // One K-step (cb, ST): refill register set ST%3 with W(s+3), MFMAs on the
+    // staged W(s) and patch(cb), then W(s+1) (set (ST+1)%3) -> the other LDS
+    // buffer.  The next patch (next channel block, or the next tile's first) is
+    // loaded at the block's first step and stored after its last.  Every
+    // load/store is unconditional (indices are clamped) so that hipcc's vmcnt
+    // bookkeeping stays exact.
+    auto step = [&](int cb, auto stc) __attribute__((always_inline)) {
+      constexpr int ST = decltype(stc)::value;
+      const int s = cb * SPC + ST;
+      int sw = s + WD;
+      if (sw >= NSTEPS) sw = more ? sw - NSTEPS : NSTEPS - 1;
+      load_w(sw, ic<ST % WD>{});
+      const bool last_cb = cb + 1 == NCB;
+      if constexpr (ST == 0 && (NCB > 1 || TPW > 1)) {
+        // next channel block, or the next tile's block 0 (clamped: this tile's
+        // block 0 again when there is no next tile, nxt == cur)
+        load_patch(last_cb ? nxt : cur, last_cb ? 0 : cb + 1);
+      }
+      const char* pb = patch + (PBUF == 2 ? ((t * NCB + cb) & 1) * PATCHB : 0);
+      const char* wb = wbuf + (gs & 1) * WB;
+      const int toff = (ST / 3) * PW + (ST % 3);
       u32x4 fa[2][TN], fb[2][TM];
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
-        if constexpr (ABL >= 2) {
-          if (s > 0) {
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) fa[g][tn] = fa0[g][tn];
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) fb[g][tm] = fb0[g][tm];
-            continue;
-          }
-        }
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
-          fa[g][tn] = *reinterpret_cast<const u32x4*>(wb + kc * WB1 + pswz(wn * WTN + tn * 16 + r16, g * 4 + q));
+          fa[g][tn] = *reinterpret_cast<const u32x4*>(wb + pswz(wn * WTN + tn * 16 + r16, g * 4 + q));
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
           fb[g][tm] = *reinterpret_cast<const u32x4*>(pb + pswz(ppix[tm] + toff, g * 4 + q));
       }
-      if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
           for (int tn = 0; tn < TN; ++tn) pmma<T>(acc[tm][tn], fa[g][tn], fb[g][tm]);
-      if constexpr (ABL >= 2) {
-        if (s == 0) {
-#pragma unroll
-          for (int g = 0; g < 2; ++g) {
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn) fa0[g][tn] = fa[g][tn];
-#pragma unroll
-            for (int tm = 0; tm < TM; ++tm) fb0[g][tm] = fb[g][tm];
+      store_w((gs + 1) & 1, ic<(ST + 1) % WD>{});
+      ++gs;
+      if constexpr (ST == SPC - 1 && (NCB > 1 || TPW > 1)) {
+        if (!last_cb || more) {
+          if constexpr (PBUF == 2) {
+            store_patch((t * NCB + cb + 1) & 1);
+            __syncthreads();
+          } else {
+            __syncthreads();  // single patch buffer: overwrite after every wave is done with it
+            store_patch(0);
+            __syncthreads();
           }
+          return;
         }
       }
-    }
-    if constexpr (ABL == 0) store_w((s + 1) & 1, ic<(ST + 1) % WD>{});
-    if constexpr (NCB > 1 && ST == SPC - 1 && ABL == 0) {
-      if constexpr (PBUF == 2) {
-        store_patch((cb + 1) & 1);
-        __syncthreads();
-      } else {
-        __syncthreads();  // single patch buffer: overwrite after every wave is done with it
-        store_patch(0);
-        __syncthreads();
-      }
-    } else {
       __syncthreads();
-    }
-  };
-  for (int cb = 0; cb < NCB; ++cb) {
-    if constexpr (TPS == 3) {
-      step(cb, ic<0>{});
-      step(cb, ic<1>{});
-      step(cb, ic<2>{});
-    } else {
+    };
+    for (int cb = 0; cb < NCB; ++cb) {
       step(cb, ic<0>{});
       step(cb, ic<1>{});
       step(cb, ic<2>{});
@@ -310,72 +297,77 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a) {
       step(cb, ic<7>{});
       step(cb, ic<8>{});
     }
-  }
 
-  // ---- epilogue straight from registers: lane holds channels co..co+3 of one pixel.
-  // All residual/bias loads are issued before any use (no serial load->use chains).
-  const T* __restrict__ res = (const T*)a.res;
-  T* __restrict__ out = (T*)a.out;
-  size_t pixo[TM];
-  bool ok[TM];
+    // ---- epilogue straight from registers: lane holds channels co..co+3 of one pixel.
+    // All residual/bias loads are issued before any use (no serial load->use chains).
+    const T* __restrict__ res = (const T*)a.res;
+    T* __restrict__ out = (T*)a.out;
+    size_t pixo[TM];
+    bool ok[TM];
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
-    const int mb = wm * WTM + tm * 16;
-    int img, y, x;
-    if constexpr (TW == 8) {
-      y = mb / 16;
-      img = o >> 3;
-      x = o & 7;
-    } else {
-      img = mb / (TH * TW);
-      y = (mb / TW) % TH;
-      x = mb % TW + o;
-    }
-    const int n = img0 + img;
-    ok[tm] = n < a.B;
-    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * Cout;
-  }
-  f32x4 bias[TN];
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + n0 + wn * WTN + tn * 16 + q * 4);
-  float rv[TM][TN][4];
-  if constexpr (EPI & EPI_RES) {
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) ld4(res + pixo[tm] + n0 + wn * WTN + tn * 16 + q * 4, rv[tm][tn]);
-  }
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
-    if (!ok[tm]) continue;
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = acc[tm][tn][j] + bias[tn][j];
-        if constexpr (EPI & EPI_RES) v[j] += rv[tm][tn][j];
-        if constexpr (EPI & EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+    for (int tm = 0; tm < TM; ++tm) {
+      const int mb = wm * WTM + tm * 16;
+      int img, y, x;
+      if constexpr (TW == 8) {
+        y = mb / 16;
+        img = o >> 3;
+        x = o & 7;
+      } else {
+        img = mb / (TH * TW);
+        y = (mb / TW) % TH;
+        x = mb % TW + o;
       }
-      st4(out + pixo[tm] + n0 + wn * WTN + tn * 16 + q * 4, v);
+      const int n = cur.img0 + img;
+      ok[tm] = n < a.B;
+      pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + cur.th0 + y) * W + cur.tw0 + x) * Cout;
     }
+    f32x4 bias[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+      bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + n0 + wn * WTN + tn * 16 + q * 4);
+    float rv[TM][TN][4];
+    if constexpr (EPI & EPI_RES) {
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) ld4(res + pixo[tm] + n0 + wn * WTN + tn * 16 + q * 4, rv[tm][tn]);
+    }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      if (!ok[tm]) continue;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = acc[tm][tn][j] + bias[tn][j];
+          if constexpr (EPI & EPI_RES) v[j] += rv[tm][tn][j];
+          if constexpr (EPI & EPI_RELU) v[j] = fmaxf(v[j], 0.f);
+        }
+        st4(out + pixo[tm] + n0 + wn * WTN + tn * 16 + q * 4, v);
+      }
+    }
+    cur = nxt;
   }
 }
 
-template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int SB = 0, int TPS = 1,
-          int WD = 3, int ABL = 0>
+template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int TPW = 1>
 static int run_patch(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "patch conv: epilogue %d", a.epi);
   PA_CHECK(a.Cin == CIN, "patch conv: Cin %d != %d", a.Cin, CIN);
   PA_CHECK(a.Hout % TH == 0 && a.Wout % TW == 0, "patch conv: %dx%d not tiled by %dx%d", a.Hout, a.Wout, TH, TW);
   PA_CHECK(a.Cout % BN == 0, "patch conv: Cout %d %% BN %d", a.Cout, BN);
-  const int tiles = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW) * (a.Cout / BN);
+  const int ntn = a.Cout / BN;
+  const int tiles = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW) * ntn;
+  // grid: a multiple of the N-tile count so a workgroup keeps its output channels
+  int grid = (tiles + TPW - 1) / TPW;
+  grid = (grid + ntn - 1) / ntn * ntn;
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES, SB, TPS, WD, ABL>), dim3(tiles),
-                       dim3(WM * WN * 64), 0, s, a);
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES, TPW>), dim3(grid),
+                       dim3(WM * WN * 64), 0, s, a, tiles);
   else
-    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU, SB, TPS, WD, ABL>), dim3(tiles),
-                       dim3(WM * WN * 64), 0, s, a);
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU, TPW>), dim3(grid),
+                       dim3(WM * WN * 64), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -400,59 +392,46 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
   if (a.Hout == 64 && a.Cout == 64) {
     if (kname) *kname = "conv3x3p_l1";
     switch (g_variant[1]) {
-      case 1: return run_patch<T, 16, 32, 1, 64, 8, 1, 1, 64, 1>(a, s);
-      case 2: return run_patch<T, 16, 32, 1, 64, 4, 1, 1, 64, 1>(a, s);
-      case 3: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0>(a, s);
-      case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 0>(a, s);
-      case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0, 1, 9>(a, s);
-      case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 0, 1, 9>(a, s);
-      case 7: return run_patch<T, 16, 32, 1, 64, 8, 1, 1, 64, 0>(a, s);
-      case 20: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0, 1, 3, 1>(a, s);
-      case 21: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0, 1, 3, 2>(a, s);
-      default: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 0>(a, s);
+      case 1: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 2>(a, s);
+      case 2: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 64, 2>(a, s);
+      case 3: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 4>(a, s);
+      case 4: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 64, 4>(a, s);
+      case 5: return run_patch<T, 16, 16, 1, 64, 8, 1, 2, 64, 4>(a, s);
+      case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 2>(a, s);
+      case 7: return run_patch<T, 16, 16, 1, 64, 8, 1, 2, 64, 2>(a, s);
+      case 8: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 1>(a, s);
+      case 9: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 4>(a, s);
+      default: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64>(a, s);
     }
   }
   if (a.Hout == 32) {
     if (kname) *kname = "conv3x3p_l2";
     switch (g_variant[2]) {
-      case 1: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 128, 1>(a, s);
-      case 2: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 128, 1>(a, s);
-      case 3: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 128, 0>(a, s);
-      case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 128, 0>(a, s);
-      case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 128, 0, 1, 9>(a, s);
-      case 6: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0, 1, 9>(a, s);
-      case 20: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0, 1, 3, 1>(a, s);
-      case 21: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0, 1, 3, 2>(a, s);
-      default: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 0>(a, s);
+      case 1: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128, 2>(a, s);
+      case 2: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 128, 2>(a, s);
+      case 3: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 128, 4>(a, s);
+      case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 2, 128, 2>(a, s);
+      case 5: return run_patch<T, 16, 16, 1, 128, 8, 1, 2, 128, 2>(a, s);
+      case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 128, 2>(a, s);
+      default: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128>(a, s);
     }
   }
   if (a.Hout == 16) {
     if (kname) *kname = "conv3x3p_l3";
     switch (g_variant[3]) {
-      case 1: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 1>(a, s);
-      case 2: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 256, 1>(a, s);
-      case 3: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 256, 0>(a, s);
-      case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 256, 0>(a, s);
-      case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 256, 0, 1, 9>(a, s);
-      case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 256, 0, 1, 9>(a, s);
-      case 20: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 0, 1, 3, 1>(a, s);
-      case 21: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 0, 1, 3, 2>(a, s);
-      default: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 0>(a, s);
+      case 1: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 2>(a, s);
+      case 2: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 256>(a, s);
+      case 3: return run_patch<T, 16, 16, 1, 32, 4, 1, 2, 256>(a, s);
+      default: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256>(a, s);
     }
   }
   if (a.Hout == 8) {
     if (kname) *kname = "conv3x3p_l4";
     switch (g_variant[4]) {
-      case 1: return run_patch<T, 8, 8, 2, 64, 2, 2, 2, 512, 1>(a, s);
-      case 2: return run_patch<T, 8, 8, 2, 64, 4, 2, 2, 512, 0>(a, s);
-      case 3: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0>(a, s);
-      case 4: return run_patch<T, 8, 8, 2, 32, 2, 2, 1, 512, 0>(a, s);
-      case 5: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0, 1, 9>(a, s);
-      case 6: return run_patch<T, 8, 8, 2, 64, 2, 2, 1, 512, 0, 1, 9>(a, s);
-      case 7: return run_patch<T, 8, 8, 2, 64, 2, 2, 2, 512, 0>(a, s);
-      case 20: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0, 1, 3, 1>(a, s);
-      case 21: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0, 1, 3, 2>(a, s);
-      default: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 0>(a, s);
+      case 1: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 2>(a, s);
+      case 2: return run_patch<T, 8, 8, 2, 64, 2, 2, 1, 512>(a, s);
+      case 3: return run_patch<T, 8, 8, 2, 64, 2, 1, 1, 512>(a, s);
+      default: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512>(a, s);
     }
   }
   set_error("patch conv: no configuration for %dx%d", a.Hout, a.Wout);

@@ -2,9 +2,10 @@
 
     python tools/layer_ab.py --variants 0 1 2 --rounds 10 [--layers 1 2 3 4]
 
-Each round runs one profiled forward (HIP events between kernels, the library's
-pa_detector_profile) per variant, variants interleaved; prints the median and min
-per (kernel, variant).
+Each round times every launch of the forward per variant (pa_detector_time_launch:
+--reps back-to-back launches between two HIP events), variants interleaved; prints
+the median and min per (launch, variant).  Outputs are checked against variant 0's
+(plain forward) before timing.
 """
 import argparse
 import os
@@ -21,6 +22,7 @@ def main():
     p.add_argument("--rounds", type=int, default=10)
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--precision", default="fp16")
+    p.add_argument("--reps", type=int, default=10)
     a = p.parse_args()
     import numpy as np
     import torch
@@ -38,14 +40,16 @@ def main():
         for v in a.variants:
             for layer in a.layers:
                 _lib.check(L.pa_debug_set_variant(layer, v))
-            prof, y = m.profile(x)
-            if ref is None:
-                ref = y
-            err = (y - ref).abs().max().item() * 127.5
             if r == 0:
-                print(f"variant {v}: max px diff vs variant {a.variants[0]} = {err:.3e}")
+                y = m(x)
+                if ref is None:
+                    ref = y
+                err = (y - ref).abs().max().item() * 127.5
+                print(f"variant {v}: max px diff vs variant {a.variants[0]} = {err:.3e}", flush=True)
                 continue  # warm-up round
-            for i, (name, ms) in enumerate(prof):
+            n = len(m.profile(x)[0])
+            for i in range(n):
+                name, ms = m.time_launch(x, i, a.reps)
                 res.setdefault(i, {}).setdefault(v, []).append((ms, name))
     tot = {v: 0.0 for v in a.variants}
     for i, d in sorted(res.items()):

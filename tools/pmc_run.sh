@@ -1,16 +1,17 @@
 #!/bin/bash
-# PMC passes over a short bench run (separate rocprofv3 invocations per counter set).
+# SQ counter passes over plain forwards (tools/pmc_forward.py), one rocprofv3 --pmc
+# invocation per counter set; summarise with tools/pmc_table.py gpurun_out/<tag>.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-pmc}
 export TMPDIR=/tmp
 cd /tmp
+O=$R/gpurun_out/$TAG
+mkdir -p $O
 run() {  # name, counters...
   local name=$1; shift
-  timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $R/gpurun_out/$TAG/$name -o p -- \
-    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --profile-passes 1 > $R/gpurun_out/$TAG/$name.log 2>&1
+  timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $O/$name -o p -- \
+    python3 $R/tools/pmc_forward.py --out $O ${FWD_ARGS} > $O/$name.log 2>&1
 }
-mkdir -p $R/gpurun_out/$TAG
 run sq1 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE && \
-run sq2 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_UNALIGNED_STALL SQ_INSTS_MFMA SQ_INSTS_VMEM_RD && \
-run fetch FETCH_SIZE && run write WRITE_SIZE
+run sq2 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_WAVES GRBM_GUI_ACTIVE
 echo rc=$?
