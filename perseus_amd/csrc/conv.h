@@ -33,11 +33,17 @@ struct ConvS2Args {
 template <typename T>
 int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname);
 
+// persistent fp16 variant (conv_s2p.hip), layer2/3
+int launch_conv3x3s2_ds_p(const ConvS2Args& a, int variant, hipStream_t s);
+
 template <typename T>
 int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);
 
 template <typename T>
 int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname);
+
+// layer1 (Cin = Cout = 64), fp16: weight-resident persistent kernel (conv_c64.hip)
+int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s);
 
 template <typename T>
 int launch_conv3x3_pipe(const ConvArgs& a, int variant, hipStream_t s);

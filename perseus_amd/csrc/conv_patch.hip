@@ -87,9 +87,15 @@ __device__ __forceinline__ int frag_off(int r) { return r < 4 ? 2 * r : (r < 12 
 template <int V>
 using ic = std::integral_constant<int, V>;
 
-template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int EPI, int TPW>
-__global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a, int ntiles) {
-  constexpr int NT = WM * WN * 64;
+// KSP = 2: intra-workgroup split-K -- two groups of WM x WN waves compute the
+// same output tile, group kg reading only channel half kg of every 64-channel
+// block (half the fragment reads per MFMA of a KSP = 1 wave with the same tile,
+// twice the waves to hide latency); group 1's accumulators are added into group
+// 0's through LDS before the epilogue.
+template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int EPI, int TPW, int KSP>
+__global__ __launch_bounds__(WM* WN * 64 * KSP) void conv3x3_patch(ConvArgs a, int ntiles) {
+  constexpr int NT = WM * WN * 64 * KSP;
+  static_assert(KSP == 1 || (KSP == 2 && TPW == 1), "split-K: one tile per workgroup");
   constexpr int KB = PElem<T>::KB;
   constexpr int CPR = 16 / sizeof(T);
   constexpr int NCB = CIN / KB;  // 128-byte channel blocks
@@ -113,12 +119,15 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a, int nti
   static_assert(SPC % WD == 0, "register-set rotation must be static");
   constexpr int PATCHB = NP * 128;
   constexpr int WB = BN * 128;  // one tap's weight tile
-  __shared__ __attribute__((aligned(16))) char smem[PBUF * PATCHB + 2 * WB];
+  constexpr int REDB = (KSP - 1) * WM * WN * TM * TN * 64 * 16;  // split-K exchange (after the K loop)
+  constexpr int STAGEB = PBUF * PATCHB + 2 * WB;
+  __shared__ __attribute__((aligned(16))) char smem[STAGEB > REDB ? STAGEB : REDB];
   char* patch = smem;
   char* wbuf = smem + PBUF * PATCHB;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int kg = wid / (WM * WN), wpos = wid - kg * (WM * WN);
+  const int wm = wpos / WN, wn = wpos - (wpos / WN) * WN;
   const int q = lane >> 4, r16 = lane & 15;
   const int H = a.Hout, W = a.Wout;
   constexpr int Cin = CIN;
@@ -253,18 +262,20 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a, int nti
       const char* pb = patch + (PBUF == 2 ? ((t * NCB + cb) & 1) * PATCHB : 0);
       const char* wb = wbuf + (gs & 1) * WB;
       const int toff = (ST / 3) * PW + (ST % 3);
-      u32x4 fa[2][TN], fb[2][TM];
+      constexpr int NG = 2 / KSP;  // 32-channel halves this wave reduces
+      u32x4 fa[NG][TN], fb[NG][TM];
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
+      for (int g = 0; g < NG; ++g) {
+        const int gc = (KSP == 2 ? kg : g) * 4 + q;
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
-          fa[g][tn] = *reinterpret_cast<const u32x4*>(wb + pswz(wn * WTN + tn * 16 + r16, g * 4 + q));
+          fa[g][tn] = *reinterpret_cast<const u32x4*>(wb + pswz(wn * WTN + tn * 16 + r16, gc));
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
-          fb[g][tm] = *reinterpret_cast<const u32x4*>(pb + pswz(ppix[tm] + toff, g * 4 + q));
+          fb[g][tm] = *reinterpret_cast<const u32x4*>(pb + pswz(ppix[tm] + toff, gc));
       }
 #pragma unroll
-      for (int g = 0; g < 2; ++g)
+      for (int g = 0; g < NG; ++g)
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -298,6 +309,22 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a, int nti
       step(cb, ic<8>{});
     }
 
+    if constexpr (KSP == 2) {
+      // the K loop ended with a barrier: the staging LDS is free for the exchange
+      f32x4* red = reinterpret_cast<f32x4*>(smem) + (size_t)wpos * TM * TN * 64 + lane;
+      if (kg == 1) {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn) red[(tm * TN + tn) * 64] = acc[tm][tn];
+      }
+      __syncthreads();
+      if (kg == 1) return;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) acc[tm][tn] += red[(tm * TN + tn) * 64];
+    }
     // ---- epilogue straight from registers: lane holds channels co..co+3 of one pixel.
     // All residual/bias loads are issued before any use (no serial load->use chains).
     const T* __restrict__ res = (const T*)a.res;
@@ -351,7 +378,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv3x3_patch(ConvArgs a, int nti
   }
 }
 
-template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int TPW = 1>
+template <typename T, int TH, int TW, int NI, int BN, int WM, int WN, int PBUF, int CIN, int TPW = 1, int KSP = 1>
 static int run_patch(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "patch conv: epilogue %d", a.epi);
   PA_CHECK(a.Cin == CIN, "patch conv: Cin %d != %d", a.Cin, CIN);
@@ -363,11 +390,11 @@ static int run_patch(const ConvArgs& a, hipStream_t s) {
   int grid = (tiles + TPW - 1) / TPW;
   grid = (grid + ntn - 1) / ntn * ntn;
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES, TPW>), dim3(grid),
-                       dim3(WM * WN * 64), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU | EPI_RES, TPW, KSP>), dim3(grid),
+                       dim3(WM * WN * 64 * KSP), 0, s, a, tiles);
   else
-    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU, TPW>), dim3(grid),
-                       dim3(WM * WN * 64), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_patch<T, TH, TW, NI, BN, WM, WN, PBUF, CIN, EPI_RELU, TPW, KSP>), dim3(grid),
+                       dim3(WM * WN * 64 * KSP), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -383,10 +410,16 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
   {
     const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : 4;
-    if (g_variant[layer] >= 10) {
+    if (g_variant[layer] >= 10 && g_variant[layer] < 30) {
       static const char* names[5] = {"", "conv3x3q_l1", "conv3x3q_l2", "conv3x3q_l3", "conv3x3q_l4"};
       if (kname) *kname = names[layer];
       return launch_conv3x3_pipe<T>(a, g_variant[layer] - 10, s);
+    }
+  }
+  if constexpr (std::is_same<T, _Float16>::value) {
+    if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && (g_variant[1] == 30 || g_variant[1] == 31)) {
+      if (kname) *kname = "conv3x3c64_l1";
+      return launch_conv3x3_c64(a, g_variant[1] - 30, s);
     }
   }
   if (a.Hout == 64 && a.Cout == 64) {
@@ -400,7 +433,7 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 2>(a, s);
       case 7: return run_patch<T, 16, 16, 1, 64, 8, 1, 2, 64, 2>(a, s);
       case 8: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 1>(a, s);
-      case 9: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 4>(a, s);
+      case 9: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 1, 2>(a, s);
       default: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64>(a, s);
     }
   }
@@ -413,6 +446,8 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 4: return run_patch<T, 16, 16, 1, 64, 8, 1, 2, 128, 2>(a, s);
       case 5: return run_patch<T, 16, 16, 1, 128, 8, 1, 2, 128, 2>(a, s);
       case 6: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 128, 2>(a, s);
+      case 7: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 128, 1, 2>(a, s);
+      case 8: return run_patch<T, 16, 16, 1, 64, 4, 1, 2, 128, 1, 2>(a, s);
       default: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 128>(a, s);
     }
   }
@@ -422,6 +457,7 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 1: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256, 2>(a, s);
       case 2: return run_patch<T, 16, 16, 1, 128, 4, 2, 2, 256>(a, s);
       case 3: return run_patch<T, 16, 16, 1, 32, 4, 1, 2, 256>(a, s);
+      case 5: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 256, 1, 2>(a, s);
       default: return run_patch<T, 16, 16, 1, 64, 4, 2, 2, 256>(a, s);
     }
   }
@@ -431,6 +467,9 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 1: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512, 2>(a, s);
       case 2: return run_patch<T, 8, 8, 2, 64, 2, 2, 1, 512>(a, s);
       case 3: return run_patch<T, 8, 8, 2, 64, 2, 1, 1, 512>(a, s);
+      case 4: return run_patch<T, 8, 8, 2, 64, 2, 1, 1, 512, 1, 2>(a, s);
+      case 5: return run_patch<T, 8, 8, 2, 64, 2, 1, 2, 512, 1, 2>(a, s);
+      case 6: return run_patch<T, 8, 8, 2, 64, 2, 2, 1, 512, 1, 2>(a, s);
       default: return run_patch<T, 8, 8, 2, 64, 4, 2, 1, 512>(a, s);
     }
   }

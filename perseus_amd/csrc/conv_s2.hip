@@ -311,6 +311,12 @@ static int run_s2(const ConvS2Args& a, hipStream_t s) {
 template <typename T>
 int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
+  if constexpr (std::is_same<T, _Float16>::value) {
+    if ((g_variant[6] == 1 || g_variant[6] == 2) && (a.Hout == 32 || a.Hout == 16)) {
+      if (kname) *kname = a.Hout == 32 ? "conv3x3s2p_l2" : "conv3x3s2p_l3";
+      return launch_conv3x3s2_ds_p(a, g_variant[6] - 1, s);
+    }
+  }
   if (a.Hout == 32) {
     if (kname) *kname = "conv3x3s2ds_l2";
     return run_s2<T, 8, 16, 1, 64, 4, 1, 64>(a, s);

@@ -21,9 +21,9 @@
 namespace pa {
 
 typedef unsigned su32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
 namespace stem {
-constexpr int PB = 8;         // pooled rows per workgroup
 constexpr int NT = 512;       // 8 waves
 constexpr int RING = 16;      // input-row ring
 constexpr int PW = 262;       // ring row width in pixels (wi = c - 3)
@@ -40,10 +40,26 @@ __device__ __forceinline__ int stem_wswz(int kh, int co, int chunk) {
 }
 __device__ __forceinline__ int crow_swz(int px, int chunk) { return px * 128 + ((chunk ^ ((px >> 1) & 7)) << 4); }
 
+template <int V>
+using stc = std::integral_constant<int, V>;
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void stem_for(F&& f) {
+  if constexpr (B < E) {
+    f(stc<B>{});
+    stem_for<B + 1, E>(f);
+  }
+}
+
+// PBT pooled rows per workgroup; D = input-row prefetch depth in conv-row pairs
+// (rows for pair j + D are loaded into registers at pair j and reach the LDS ring
+// at the end of pair j + D - 1), so D x 16 KB of input is in flight per CU.
+template <int PBT, int D>
 __global__ __launch_bounds__(512) void stem_pool_fp16(const float* __restrict__ x, int B, int Cin,
                                                       const _Float16* __restrict__ w, const float* __restrict__ bias,
                                                       _Float16* __restrict__ out) {
   using namespace stem;
+  static_assert(RING >= 9 + 4 && D >= 1 && D <= 3, "ring / prefetch depth");
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   char* ring = smem;
   char* wl = smem + RING * ROWB;
@@ -52,7 +68,7 @@ __global__ __launch_bounds__(512) void stem_pool_fp16(const float* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = lane >> 4, r16 = lane & 15;
   const int n = blockIdx.y;
-  const int p0 = blockIdx.x * PB;
+  const int p0 = blockIdx.x * PBT;
   const float* xn = x + (size_t)n * Cin * 256 * 256;
 
   // ---- weights [64][7][32] fp16 (global) -> LDS [kh][co][4 swizzled chunks]
@@ -62,34 +78,31 @@ __global__ __launch_bounds__(512) void stem_pool_fp16(const float* __restrict__ 
         *reinterpret_cast<const su32x4*>(w + (size_t)co * 224 + kh * 32 + ch * 8);
   }
 
-  // ---- input rows: thread t < 256 owns (row t/64 of the 4 new rows, 4 columns)
+  // ---- 4 input rows per pair: thread t -> row (t >> 7), pixels 4*((t >> 1) & 63)..+3,
+  // channels 2*(t & 1), 2*(t & 1) + 1 (two float4 loads, 4 x 4-byte LDS stores)
+  const int lr = tid >> 7, lcg = (tid >> 1) & 63, lcp = tid & 1;
   auto load_rows = [&](int hi0, float4* v) __attribute__((always_inline)) {
-    const int r = tid >> 6, cg = tid & 63;
-    const int hi = hi0 + r;
+    const int hi = hi0 + lr;
     const bool ok = (unsigned)hi < 256u;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < 2; ++c) {
+      const int ch = 2 * lcp + c;
       v[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok && c < Cin) v[c] = *reinterpret_cast<const float4*>(xn + ((size_t)c * 256 + hi) * 256 + cg * 4);
+      if (ok && ch < Cin) v[c] = *reinterpret_cast<const float4*>(xn + ((size_t)ch * 256 + hi) * 256 + lcg * 4);
     }
   };
   auto store_rows = [&](int hi0, const float4* v) __attribute__((always_inline)) {
-    const int r = tid >> 6, cg = tid & 63;
-    const int slot = (hi0 + r + 64) & (RING - 1);
-    char* row = ring + slot * ROWB;
-    // 4 pixels x 4 channels -> 32 contiguous bytes at pixel (cg*4 + 3)
-    _Float16 h[16];
-    h[0] = (_Float16)v[0].x; h[1] = (_Float16)v[1].x; h[2] = (_Float16)v[2].x; h[3] = (_Float16)v[3].x;
-    h[4] = (_Float16)v[0].y; h[5] = (_Float16)v[1].y; h[6] = (_Float16)v[2].y; h[7] = (_Float16)v[3].y;
-    h[8] = (_Float16)v[0].z; h[9] = (_Float16)v[1].z; h[10] = (_Float16)v[2].z; h[11] = (_Float16)v[3].z;
-    h[12] = (_Float16)v[0].w; h[13] = (_Float16)v[1].w; h[14] = (_Float16)v[2].w; h[15] = (_Float16)v[3].w;
-    // pixel cg*4+3 starts at byte (cg*4+3)*8: only 8-B aligned -> 4 x 8-B stores
-    uint2* d = reinterpret_cast<uint2*>(row + (cg * 4 + 3) * 8);
-    const uint2* s = reinterpret_cast<const uint2*>(h);
-    d[0] = s[0];
-    d[1] = s[1];
-    d[2] = s[2];
-    d[3] = s[3];
+    const int slot = (hi0 + lr + 64) & (RING - 1);
+    char* row = ring + slot * ROWB + (lcg * 4 + 3) * 8 + lcp * 4;
+    const float a0[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
+    const float a1[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      half2_t h;
+      h.x = (_Float16)a0[k];
+      h.y = (_Float16)a1[k];
+      *reinterpret_cast<half2_t*>(row + k * 8) = h;
+    }
   };
   // zero the 3 left / 3 right pad pixels of every ring row once (never rewritten)
   for (int i = tid; i < RING * 6; i += NT) {
@@ -97,31 +110,37 @@ __global__ __launch_bounds__(512) void stem_pool_fp16(const float* __restrict__ 
     const int px = k < 3 ? k : 256 + k;  // 0,1,2 and 259,260,261
     *reinterpret_cast<uint2*>(ring + slot * ROWB + px * 8) = make_uint2(0, 0);
   }
-  // prologue: the 9 input rows of pair 0 (hi = 4*p0 - 7 .. 4*p0 + 1)
+  // prologue: the 9 input rows of pair 0 (hi = 4*p0 - 7 .. 4*p0 + 1) straight to the ring
   const int hbase = 4 * p0 - 7;
   {
-    float4 v[4];
+    float4 v[2];
+#pragma unroll
     for (int k = 0; k < 9; k += 4) {
-      if (tid < 256 && (tid >> 6) + k < 9) {
+      if (lr + k < 9) {
         load_rows(hbase + k, v);
         store_rows(hbase + k, v);
       }
     }
   }
+  // register prefetch sets: set (j % D) holds the 4 rows of pair j + D... loaded at pair j
+  float4 pf[D][2];
+#pragma unroll
+  for (int k = 1; k < D; ++k) load_rows(hbase + 9 + 4 * (k - 1), pf[k]);  // pairs 1..D-1: rows needed by pair k
   __syncthreads();
 
   // wave w: pixels [32w, 32w+32) of the pair (conv row w>>2, cols (w&3)*32..), all 64 channels
   constexpr int TM = 2, TN = 4;
   const int hr = wid >> 2, wo0 = (wid & 3) * 32;
-  float4 nv[4];
   f32x4 bv[TN];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) bv[tn] = *reinterpret_cast<const f32x4*>(bias + tn * 16 + q * 4);
 
-  for (int j = 0; j <= PB; ++j) {
+  stem_for<0, PBT + 1>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
     const int r0 = 2 * p0 - 2 + 2 * j;  // conv rows r0, r0+1
     const int hs = 4 * p0 - 7 + 4 * j;  // first input row of this pair
-    if (j < PB && tid < 256) load_rows(hs + 9, nv);
+    // rows of pair j + D (first row hs + 9 + 4 (D - 1)) -> set j % D
+    if constexpr (j + D <= PBT) load_rows(hs + 9 + 4 * (D - 1), pf[j % D]);
     f32x4 acc[TM][TN];
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -166,9 +185,10 @@ __global__ __launch_bounds__(512) void stem_pool_fp16(const float* __restrict__ 
         }
       }
     }
-    if (j < PB && tid < 256) store_rows(hs + 9, nv);
+    // rows of pair j + 1 (loaded at pair j + 1 - D into set (j + 1) % D) -> ring
+    if constexpr (j < PBT) store_rows(hs + 9, pf[(j + 1) % D]);
     __syncthreads();  // (B) conv rows + next input rows visible
-    if (j >= 1) {
+    if constexpr (j >= 1) {
       // pooled row p = p0 + j - 1 from conv rows 2p-1, 2p, 2p+1 (= r0-1, r0, r0+1)
       const int p = p0 + j - 1;
       const int qc = tid >> 3, c8 = tid & 7;
@@ -192,16 +212,29 @@ __global__ __launch_bounds__(512) void stem_pool_fp16(const float* __restrict__ 
       for (int e = 0; e < 8; ++e) o[e] = (_Float16)m[e];
       *reinterpret_cast<half8*>(out + (((size_t)n * 64 + p) * 64 + qc) * 64 + c8 * 8) = o;
     }
-  }
+  });
+}
+
+template <int PBT, int D>
+static int run_stem(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,
+                    hipStream_t s) {
+  hipLaunchKernelGGL((stem_pool_fp16<PBT, D>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
 }
 
 int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,
                           hipStream_t s) {
   PA_CHECK(Cin >= 1 && Cin <= 4, "stem: Cin %d", Cin);
   if (B <= 0) return PA_OK;
-  hipLaunchKernelGGL(stem_pool_fp16, dim3(64 / stem::PB, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out);
-  PA_LAUNCH_CHECK();
-  return PA_OK;
+  switch (g_variant[0]) {
+    case 1: return run_stem<8, 1>(x, B, Cin, w, bias, out, s);
+    case 2: return run_stem<8, 3>(x, B, Cin, w, bias, out, s);
+    case 3: return run_stem<16, 2>(x, B, Cin, w, bias, out, s);
+    case 4: return run_stem<16, 3>(x, B, Cin, w, bias, out, s);
+    case 5: return run_stem<4, 2>(x, B, Cin, w, bias, out, s);
+    default: return run_stem<8, 2>(x, B, Cin, w, bias, out, s);
+  }
 }
 
 }  // namespace pa
