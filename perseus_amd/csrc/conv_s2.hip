@@ -312,9 +312,10 @@ template <typename T>
 int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
   if constexpr (std::is_same<T, _Float16>::value) {
-    if ((g_variant[6] == 1 || g_variant[6] == 2) && (a.Hout == 32 || a.Hout == 16)) {
+    // layer2/3: persistent kernel (g_variant[6] = 3 selects the one-tile kernel below)
+    if (g_variant[6] != 3 && (a.Hout == 32 || a.Hout == 16)) {
       if (kname) *kname = a.Hout == 32 ? "conv3x3s2p_l2" : "conv3x3s2p_l3";
-      return launch_conv3x3s2_ds_p(a, g_variant[6] - 1, s);
+      return launch_conv3x3s2_ds_p(a, g_variant[6] == 2 ? 1 : 0, s);
     }
   }
   if (a.Hout == 32) {

@@ -231,9 +231,8 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     case 1: return run_stem<8, 1>(x, B, Cin, w, bias, out, s);
     case 2: return run_stem<8, 3>(x, B, Cin, w, bias, out, s);
     case 3: return run_stem<16, 2>(x, B, Cin, w, bias, out, s);
-    case 4: return run_stem<16, 3>(x, B, Cin, w, bias, out, s);
-    case 5: return run_stem<4, 2>(x, B, Cin, w, bias, out, s);
-    default: return run_stem<8, 2>(x, B, Cin, w, bias, out, s);
+    case 4: return run_stem<32, 3>(x, B, Cin, w, bias, out, s);
+    default: return run_stem<16, 3>(x, B, Cin, w, bias, out, s);
   }
 }
 

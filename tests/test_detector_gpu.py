@@ -139,8 +139,29 @@ def test_profile_reports_every_kernel():
     names = [n for n, _ in prof]
     assert names[0] == "stem_conv7x7_pool" and names[-1] == "avgpool_fc"  # fp16: stem + maxpool fused
     assert len(names) == 1 + 4 + 4 + 4 + 4 + 1  # stride-2 conv1 + 1x1 downsample fused
-    assert names[5].startswith("conv3x3s2ds")
+    assert names[5].startswith("conv3x3s2")
     assert torch.equal(y, m(x))
     m.precision = "fp32"
     prof32, _ = m.profile(x)
     assert [n for n, _ in prof32][:2] == ["stem_conv7x7", "maxpool"]
+
+
+@pytest.mark.parametrize("B", [1, 3, 64])
+def test_kernel_variants_agree_bit_for_bit(B):
+    """The persistent kernels (layer1 weight-resident conv, stride-2 + downsample)
+    and the one-tile-per-workgroup kernels they replace accumulate in the same order:
+    identical outputs, at batches below and above one tile per CU."""
+    from perseus_amd import _lib
+
+    L = _lib.lib()
+    m = model(0)
+    x = torch.from_numpy(synth.synthetic_frames(2, B)).cuda()
+    y0 = m(x)
+    try:
+        for layer, variant in ((1, 3), (6, 3), (0, 1)):
+            _lib.check(L.pa_debug_set_variant(layer, variant))
+        y1 = m(x)
+    finally:
+        for layer in range(8):
+            L.pa_debug_set_variant(layer, 0)
+    assert torch.equal(y0, y1)
