@@ -137,8 +137,15 @@ def main():
             if dur and roof.get("kernel"):
                 idx = [i for i, nm in enumerate(names) if nm == roof["kernel"]]
                 rp = sum(dur[i] for i in idx) / len(idx)
-                lines.append(f"Agreement: bench roofline kernel `{roof['kernel']}` avg {roof['avg_ms'] * 1e3:.2f} us "
-                             f"(HIP events, back-to-back reps) vs rocprofv3 kernel-trace {rp:.2f} us per launch.")
+                line_ = (f"Agreement: bench roofline kernel `{roof['kernel']}` avg {roof['avg_ms'] * 1e3:.2f} us per "
+                         f"launch (HIP events, back-to-back reps)")
+                if stats and syms:
+                    avg = {r["Name"]: float(r["AverageNs"]) / 1e3 for r in csv.DictReader(open(stats))}
+                    if all(syms[i] in avg for i in idx):
+                        st = sum(avg[syms[i]] for i in idx) / len(idx)
+                        line_ += f"; rocprofv3 --stats of the same bench command: {st:.2f} us"
+                line_ += f"; kernel trace of plain forwards (cold-er caches): {rp:.2f} us."
+                lines.append(line_)
     if fb:
         tf = os.path.join(out, "pmc_traffic.json")
         allt = json.load(open(tf)) if os.path.exists(tf) else {}
