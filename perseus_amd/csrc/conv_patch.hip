@@ -417,6 +417,17 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
     }
   }
   if constexpr (std::is_same<T, _Float16>::value) {
+    const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : 4;
+    // layers 2-4: LDS-DMA kernel (measured 5-13 % under the register-staged one);
+    // shipped configs: layer2 plain, layers 3/4 with the fragment prefetch
+    const int gv = g_variant[layer] >= 40 && g_variant[layer] <= 43 ? g_variant[layer] - 40
+                   : g_variant[layer] == 0 && layer >= 2                ? (layer == 2 ? 0 : 2)
+                                                                         : -1;
+    if (gv >= 0) {
+      static const char* names[5] = {"", "conv3x3g_l1", "conv3x3g_l2", "conv3x3g_l3", "conv3x3g_l4"};
+      if (kname) *kname = names[layer];
+      return launch_conv3x3_glds(a, gv, s);
+    }
     // layer1: the weight-resident persistent kernel for conv1 of each block (no
     // residual); conv2 (+ residual) measured equal on both kernels, keeps the patch one
     const bool c64 = g_variant[1] == 30 || g_variant[1] == 31 || (g_variant[1] == 0 && !(a.epi & EPI_RES));

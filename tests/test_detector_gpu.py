@@ -158,7 +158,7 @@ def test_kernel_variants_agree_bit_for_bit(B):
     x = torch.from_numpy(synth.synthetic_frames(2, B)).cuda()
     y0 = m(x)
     try:
-        for layer, variant in ((1, 3), (6, 3), (0, 1)):
+        for layer, variant in ((1, 3), (2, 1), (3, 1), (4, 1), (6, 3), (0, 1)):
             _lib.check(L.pa_debug_set_variant(layer, variant))
         y1 = m(x)
     finally:
