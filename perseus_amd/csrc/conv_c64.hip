@@ -44,6 +44,13 @@ constexpr int WBYTES = WROWS * 128;                     // 73,728 B
 
 __device__ __forceinline__ int c64swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 __device__ __forceinline__ int c64frag(int r) { return r < 4 ? 2 * r : (r < 12 ? 2 * (r - 4) + 1 : 2 * (r - 8)); }
+// Output-channel order of the weight rows inside each group of 32: LDS row
+// rho = 16 t + 4 q + v (MFMA tile t of a pair, lane quad q, accumulator slot v)
+// holds channel 8 q + 4 t + v, so a lane's two tiles of a pair cover 8
+// consecutive channels of its pixel -> 16-byte residual loads and output stores.
+__device__ __forceinline__ int c64perm(int rho) {
+  return (rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);
+}
 
 template <int WM, int EPI>
 __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
@@ -77,7 +84,7 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
         if (h * HALF + i < WCH) {
           const int row = c >> 3, ch = c & 7;
           const int tap = row >> 6, co = row & 63;
-          v[i] = *reinterpret_cast<const c64u4*>(w + (size_t)co * 576 + tap * 64 + ch * 8);
+          v[i] = *reinterpret_cast<const c64u4*>(w + (size_t)c64perm(co) * 576 + tap * 64 + ch * 8);
         }
       }
 #pragma unroll
@@ -119,9 +126,10 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
     const int mb = wm * WTM + tm * 16;
     ppix[tm] = (mb / TW) * PW + mb % TW + o;
   }
+  // lane's channels for tile pair p: 32 p + 8 q + [0, 8)
   f32x4 bias[TN];
 #pragma unroll
-  for (int tn = 0; tn < TN; ++tn) bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + tn * 16 + q * 4);
+  for (int tn = 0; tn < TN; ++tn) bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4);
 
   int tile = blockIdx.x;
   load_patch(tile);
@@ -141,17 +149,17 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
       const int mb = wm * WTM + tm * 16;
       pixo[tm] = (((size_t)img * H + th0 + mb / TW) * W + tw0 + mb % TW + o) * 64;
     }
-    float rv[TM][TN][4];
+    // residual issued now, kept raw: converting here would make the MFMAs below
+    // wait for it (and, vmcnt being in order, for the next patch's loads)
+    half8 rv[TM][TN / 2];
     if constexpr (EPI & EPI_RES) {
       const _Float16* __restrict__ res = (const _Float16*)a.res;
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          half4 hv = *reinterpret_cast<const half4*>(res + pixo[tm] + tn * 16 + q * 4);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) rv[tm][tn][j] = (float)hv[j];
-        }
+        for (int p = 0; p < TN / 2; ++p) rv[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + p * 32 + q * 8);
+      // keep them here: the scheduler would otherwise sink them next to their use
+      __builtin_amdgcn_sched_barrier(0);
     }
 
     f32x4 acc[TM][TN];
@@ -194,16 +202,16 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        half4 hv;
+      for (int p = 0; p < TN / 2; ++p) {
+        half8 hv;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float v = acc[tm][tn][j] + bias[tn][j];
-          if constexpr (EPI & EPI_RES) v += rv[tm][tn][j];
+        for (int j = 0; j < 8; ++j) {
+          float v = acc[tm][2 * p + (j >> 2)][j & 3] + bias[2 * p + (j >> 2)][j & 3];
+          if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
           v = fmaxf(v, 0.f);
           hv[j] = (_Float16)v;
         }
-        *reinterpret_cast<half4*>(out + pixo[tm] + tn * 16 + q * 4) = hv;
+        *reinterpret_cast<half8*>(out + pixo[tm] + p * 32 + q * 8) = hv;
       }
 
     // next tile's patch into the other buffer (last read during tile t-1, before

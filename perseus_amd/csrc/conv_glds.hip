@@ -29,6 +29,12 @@ __device__ __attribute__((aligned(128))) unsigned g_zero_line[32];  // 128 zero 
 
 __device__ __forceinline__ int gswz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 __device__ __forceinline__ int gfrag(int r) { return r < 4 ? 2 * r : (r < 12 ? 2 * (r - 4) + 1 : 2 * (r - 8)); }
+// weight-row -> output-channel order inside each group of 32 rows: row 16 t + 4 q + v
+// holds channel 8 q + 4 t + v, so the accumulators of a lane's tile pair (t = 0, 1)
+// are 8 consecutive channels of one pixel (16-byte residual loads / output stores)
+__device__ __forceinline__ int gperm(int rho) {
+  return (rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);
+}
 
 // The LDS-DMA / s_waitcnt builtins exist only for the device target; without the
 // guard the host pass silently drops the kernel's launch stub.
@@ -70,6 +76,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_glds(ConvArgs a) {
   static_assert(BN * 8 % NT == 0 && WDMA >= 1, "weight tile / threads");
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
   static_assert(TW >= 16 || (TW == 8 && NI == 2), "fragment geometry");
+  static_assert(WTN % 32 == 0, "channel-pair permutation needs 32-channel wave tiles");
+  // epilogue loads issued during the last block: bias (TN) + residual (TM * TN / 2)
+  constexpr int RL = TN + ((EPI & EPI_RES) ? TM * TN / 2 : 0);
   constexpr int NSLOT = FP ? 4 : 3;
   __shared__ __attribute__((aligned(1024))) char smem[2 * PATCHB + NSLOT * WB];
   char* patch = smem;
@@ -119,7 +128,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_glds(ConvArgs a) {
   for (int i = 0; i < WDMA; ++i) {
     const int c = (i * NW + wid) * 64 + lane;
     const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
-    wsrc[i] = w + (size_t)(n0 + co) * KTOT + lc * 8;
+    wsrc[i] = w + (size_t)(n0 + gperm(co)) * KTOT + lc * 8;
   }
   auto dma_w = [&](int s, int slot) __attribute__((always_inline)) {
     const int cb = s / 9, tap = s - (s / 9) * 9;
@@ -140,6 +149,45 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_glds(ConvArgs a) {
     }
   }
 
+  // epilogue addressing (needed early: the residual is prefetched during the last block)
+  const _Float16* __restrict__ res = (const _Float16*)a.res;
+  _Float16* __restrict__ out = (_Float16*)a.out;
+  size_t pixo[TM];
+  bool ok[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int mb = wm * WTM + tm * 16;
+    int img, y, x;
+    if constexpr (TW == 8) {
+      y = mb / 16;
+      img = o >> 3;
+      x = o & 7;
+    } else {
+      img = mb / (TH * TW);
+      y = (mb / TW) % TH;
+      x = mb % TW + o;
+    }
+    const int n = img0 + img;
+    ok[tm] = n < a.B;
+    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * Cout + n0 + wn * WTN + q * 8;
+  }
+  // bias + residual: RL loads issued right after the DMAs of the last block's
+  // first step.  vmcnt is in order, so the waits of that step and the next (the
+  // only ones whose awaited DMA is older than these loads) count them too.
+  half8 rv[TM][TN / 2];
+  f32x4 bias[TN];
+  auto load_res = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+      bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + n0 + wn * WTN + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4);
+    if constexpr (EPI & EPI_RES) {
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int p = 0; p < TN / 2; ++p) rv[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + p * 32);
+    }
+  };
+
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -156,63 +204,70 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_glds(ConvArgs a) {
 
     // step s = (cb, TAP): DMA W(s+2) (and at TAP 0 the next block's patch), MFMAs on
     // W(s) / patch(cb), then wait for W(s+1) [+ patch(cb+1) after TAP 8] and barrier.
-    auto step = [&](int cb, auto tapc) __attribute__((always_inline)) {
+    // LB: cb is the last block (residual prefetch at TAP 0; no wait after TAP 8).
+    auto step = [&](int cb, auto tapc, auto lbc) __attribute__((always_inline)) {
       constexpr int TAP = decltype(tapc)::value;
+      constexpr bool LB = decltype(lbc)::value;
+      constexpr int X = (LB && TAP <= 1) ? RL : 0;
       const int s = cb * 9 + TAP;
       const bool wpre = s + 2 < NSTEPS;
       if (wpre) dma_w(s + 2, (s + 2) % 3);
       const bool ppre = TAP == 0 && cb + 1 < NCB;
       if (ppre) dma_patch(cb + 1, (cb + 1) & 1);
+      if constexpr (LB && TAP == 0) load_res();
       const char* pb = patch + (cb & 1) * PATCHB;
       const char* wb = wring + (s % 3) * WB;
       constexpr int TOFF = (TAP / 3) * PW + (TAP % 3);
       gu4 fa[2][TN], fb[2][TM];
-  #pragma unroll
+#pragma unroll
       for (int g = 0; g < 2; ++g) {
-  #pragma unroll
+#pragma unroll
         for (int tn = 0; tn < TN; ++tn)
           fa[g][tn] = *reinterpret_cast<const gu4*>(wb + gswz(wn * WTN + tn * 16 + r16, g * 4 + q));
-  #pragma unroll
+#pragma unroll
         for (int tm = 0; tm < TM; ++tm)
           fb[g][tm] = *reinterpret_cast<const gu4*>(pb + gswz(ppix[tm] + TOFF, g * 4 + q));
       }
       __builtin_amdgcn_s_setprio(1);
-  #pragma unroll
+#pragma unroll
       for (int g = 0; g < 2; ++g)
-  #pragma unroll
+#pragma unroll
         for (int tm = 0; tm < TM; ++tm)
-  #pragma unroll
+#pragma unroll
           for (int tn = 0; tn < TN; ++tn)
             acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[g][tn]),
                                                                  __builtin_bit_cast(half8, fb[g][tm]), acc[tm][tn], 0, 0,
                                                                  0);
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (LB && TAP == 8) return;  // fragments are in registers; nothing left to land
       // W(s+1) was issued one step ago; after it: this step's W(s+2) DMAs and, at TAP 0,
       // the patch DMAs; at TAP 1 the patch DMAs issued at TAP 0 are after it too.
       // Before the last tap of a block everything (incl. the next patch) must land.
       if (!wpre) {
-        wait_vm<0>();
+        wait_vm<X>();
       } else if constexpr (TAP == 0 || TAP == 1) {
         if (cb + 1 < NCB)
-          wait_vm<WDMA + PDMA>();
+          wait_vm<WDMA + PDMA + X>();
         else
-          wait_vm<WDMA>();
+          wait_vm<WDMA + X>();
       } else {
         wait_vm<WDMA>();
       }
       __builtin_amdgcn_s_barrier();
     };
-    for (int cb = 0; cb < NCB; ++cb) {
-      step(cb, gic<0>{});
-      step(cb, gic<1>{});
-      step(cb, gic<2>{});
-      step(cb, gic<3>{});
-      step(cb, gic<4>{});
-      step(cb, gic<5>{});
-      step(cb, gic<6>{});
-      step(cb, gic<7>{});
-      step(cb, gic<8>{});
-    }
+    auto block = [&](int cb, auto lbc) __attribute__((always_inline)) {
+      step(cb, gic<0>{}, lbc);
+      step(cb, gic<1>{}, lbc);
+      step(cb, gic<2>{}, lbc);
+      step(cb, gic<3>{}, lbc);
+      step(cb, gic<4>{}, lbc);
+      step(cb, gic<5>{}, lbc);
+      step(cb, gic<6>{}, lbc);
+      step(cb, gic<7>{}, lbc);
+      step(cb, gic<8>{}, lbc);
+    };
+    for (int cb = 0; cb < NCB - 1; ++cb) block(cb, std::false_type{});
+    block(NCB - 1, std::true_type{});
   } else {
     // prologue: patch(0), W(0..2) resident
     dma_patch(0, 0);
@@ -240,13 +295,16 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_glds(ConvArgs a) {
     };
     read_frags(0, gic<0>{}, gic<0>{});
     // step (cb, TAP) with fragment set PAR = s & 1 (static: cb pairs are unrolled)
-    auto step = [&](int cb, auto tapc, auto parc) __attribute__((always_inline)) {
+    auto step = [&](int cb, auto tapc, auto parc, auto lbc) __attribute__((always_inline)) {
       constexpr int TAP = decltype(tapc)::value, PAR = decltype(parc)::value;
+      constexpr bool LB = decltype(lbc)::value;
+      constexpr int X = (LB && TAP <= 1) ? RL : 0;
       const int s = cb * 9 + TAP;
       const bool wpre = s + 3 < NSTEPS;
       if (wpre) dma_w(s + 3, (s + 3) & 3);
       const bool ppre = TAP == 0 && cb + 1 < NCB;
       if (ppre) dma_patch(cb + 1, (cb + 1) & 1);
+      if constexpr (LB && TAP == 0) load_res();
       if (s + 1 < NSTEPS) {
         if constexpr (TAP < 8)
           read_frags(cb, gic<TAP + 1>{}, gic<PAR ^ 1>{});
@@ -264,19 +322,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_glds(ConvArgs a) {
                                                                  __builtin_bit_cast(half8, fb[PAR][g][tm]),
                                                                  acc[tm][tn], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
+      if constexpr (LB && TAP == 8) return;  // nothing left to land or to protect
       // W(s+2) (read as fragments during step s+1) must have landed; after it were
       // issued: W(s+3) (this step) and, at TAP 0/1, the next block's patch.  The
       // patch itself is retired at TAP 7 (issued before W(s+2) there).
       if constexpr (TAP == 0 || TAP == 1) {
         if (cb + 1 < NCB) {
           if (wpre)
-            wait_vm<WDMA + PDMA>();
+            wait_vm<WDMA + PDMA + X>();
           else
-            wait_vm<PDMA>();
+            wait_vm<PDMA + X>();
         } else if (wpre) {
-          wait_vm<WDMA>();
+          wait_vm<WDMA + X>();
         } else {
-          wait_vm<0>();
+          wait_vm<X>();
         }
       } else {
         if (wpre)
@@ -286,78 +345,48 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_glds(ConvArgs a) {
       }
       __builtin_amdgcn_s_barrier();
     };
-    auto block = [&](int cb, auto par0) __attribute__((always_inline)) {
+    auto block = [&](int cb, auto par0, auto lbc) __attribute__((always_inline)) {
       constexpr int P0 = decltype(par0)::value;
-      step(cb, gic<0>{}, gic<P0>{});
-      step(cb, gic<1>{}, gic<P0 ^ 1>{});
-      step(cb, gic<2>{}, gic<P0>{});
-      step(cb, gic<3>{}, gic<P0 ^ 1>{});
-      step(cb, gic<4>{}, gic<P0>{});
-      step(cb, gic<5>{}, gic<P0 ^ 1>{});
-      step(cb, gic<6>{}, gic<P0>{});
-      step(cb, gic<7>{}, gic<P0 ^ 1>{});
-      step(cb, gic<8>{}, gic<P0>{});
+      step(cb, gic<0>{}, gic<P0>{}, lbc);
+      step(cb, gic<1>{}, gic<P0 ^ 1>{}, lbc);
+      step(cb, gic<2>{}, gic<P0>{}, lbc);
+      step(cb, gic<3>{}, gic<P0 ^ 1>{}, lbc);
+      step(cb, gic<4>{}, gic<P0>{}, lbc);
+      step(cb, gic<5>{}, gic<P0 ^ 1>{}, lbc);
+      step(cb, gic<6>{}, gic<P0>{}, lbc);
+      step(cb, gic<7>{}, gic<P0 ^ 1>{}, lbc);
+      step(cb, gic<8>{}, gic<P0>{}, lbc);
     };
     if constexpr (NCB == 1) {
-      block(0, gic<0>{});
+      block(0, gic<0>{}, std::true_type{});
     } else {
-      for (int cb = 0; cb < NCB; cb += 2) {
-        block(cb, gic<0>{});
-        block(cb + 1, gic<1>{});
+      static_assert(NCB % 2 == 0, "FP blocks run in pairs");
+      for (int cb = 0; cb < NCB - 2; cb += 2) {
+        block(cb, gic<0>{}, std::false_type{});
+        block(cb + 1, gic<1>{}, std::false_type{});
       }
+      block(NCB - 2, gic<0>{}, std::false_type{});
+      block(NCB - 1, gic<1>{}, std::true_type{});
     }
   }
 
-  // ---- epilogue from registers
-  const _Float16* __restrict__ res = (const _Float16*)a.res;
-  _Float16* __restrict__ out = (_Float16*)a.out;
-  size_t pixo[TM];
-  bool ok[TM];
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
-    const int mb = wm * WTM + tm * 16;
-    int img, y, x;
-    if constexpr (TW == 8) {
-      y = mb / 16;
-      img = o >> 3;
-      x = o & 7;
-    } else {
-      img = mb / (TH * TW);
-      y = (mb / TW) % TH;
-      x = mb % TW + o;
-    }
-    const int n = img0 + img;
-    ok[tm] = n < a.B;
-    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * Cout;
-  }
-  f32x4 bias[TN];
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + n0 + wn * WTN + tn * 16 + q * 4);
-  half4 rv[TM][TN];
-  if constexpr (EPI & EPI_RES) {
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn)
-        rv[tm][tn] = *reinterpret_cast<const half4*>(res + pixo[tm] + n0 + wn * WTN + tn * 16 + q * 4);
-  }
+  // ---- epilogue from registers: lane's channels per tile pair p are pixo + 32 p + [0, 8)
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     if (!ok[tm]) continue;
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      half4 hv;
+    for (int p = 0; p < TN / 2; ++p) {
+      half8 hv;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float v = acc[tm][tn][j] + bias[tn][j];
-        if constexpr (EPI & EPI_RES) v += (float)rv[tm][tn][j];
+      for (int j = 0; j < 8; ++j) {
+        float v = acc[tm][2 * p + (j >> 2)][j & 3] + bias[2 * p + (j >> 2)][j & 3];
+        if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
         hv[j] = (_Float16)fmaxf(v, 0.f);
       }
-      *reinterpret_cast<half4*>(out + pixo[tm] + n0 + wn * WTN + tn * 16 + q * 4) = hv;
+      *reinterpret_cast<half8*>(out + pixo[tm] + p * 32) = hv;
     }
   }
 }
-
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int FP = 0>
 static int run_glds(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "glds conv: epilogue %d", a.epi);

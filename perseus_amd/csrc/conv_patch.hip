@@ -428,9 +428,9 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       if (kname) *kname = names[layer];
       return launch_conv3x3_glds(a, gv, s);
     }
-    // layer1: the weight-resident persistent kernel for conv1 of each block (no
-    // residual); conv2 (+ residual) measured equal on both kernels, keeps the patch one
-    const bool c64 = g_variant[1] == 30 || g_variant[1] == 31 || (g_variant[1] == 0 && !(a.epi & EPI_RES));
+    // layer1: the weight-resident persistent kernel for all four convs (variant 32
+    // keeps the patch kernel for reference timing)
+    const bool c64 = g_variant[1] == 30 || g_variant[1] == 31 || g_variant[1] == 0;
     if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && c64) {
       if (kname) *kname = "conv3x3c64_l1";
       return launch_conv3x3_c64(a, g_variant[1] == 31 ? 1 : 0, s);
@@ -448,6 +448,7 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       case 7: return run_patch<T, 16, 16, 1, 64, 8, 1, 2, 64, 2>(a, s);
       case 8: return run_patch<T, 16, 16, 1, 64, 8, 1, 1, 64, 1>(a, s);
       case 9: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64, 1, 2>(a, s);
+      case 32:
       default: return run_patch<T, 16, 16, 1, 64, 4, 1, 1, 64>(a, s);
     }
   }
