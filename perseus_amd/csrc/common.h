@@ -41,6 +41,14 @@ void set_error(const char* fmt, ...);
     }                                                                                  \
   } while (0)
 
+// Workgroup barrier that orders LDS only: lgkmcnt(0) + s_barrier.  __syncthreads()
+// also waits vmcnt(0), which would drain every global prefetch in flight.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // kornia.geometry.conversions.denormalize_pixel_coordinates in f32, operation for
 // operation: factor = 2 / (S - 1); px = (1 / factor) * (n + 1).  (1 / f32(2/255) is
 // 127.49999237, not 127.5: the reference's pixels carry that rounding.)

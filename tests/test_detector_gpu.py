@@ -150,7 +150,8 @@ def test_profile_reports_every_kernel():
 def test_kernel_variants_agree_bit_for_bit(B):
     """The persistent kernels (layer1 weight-resident conv, stride-2 + downsample)
     and the one-tile-per-workgroup kernels they replace accumulate in the same order:
-    identical outputs, at batches below and above one tile per CU."""
+    identical outputs, at batches below and above one tile per CU.  (Stem variant 10
+    is the same stem kernel at a different band height.)"""
     from perseus_amd import _lib
 
     L = _lib.lib()
@@ -158,7 +159,7 @@ def test_kernel_variants_agree_bit_for_bit(B):
     x = torch.from_numpy(synth.synthetic_frames(2, B)).cuda()
     y0 = m(x)
     try:
-        for layer, variant in ((1, 3), (2, 1), (3, 1), (4, 1), (6, 3), (0, 1)):
+        for layer, variant in ((1, 3), (2, 1), (3, 1), (4, 1), (6, 3), (0, 10)):
             _lib.check(L.pa_debug_set_variant(layer, variant))
         y1 = m(x)
     finally:
