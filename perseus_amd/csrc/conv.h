@@ -45,6 +45,11 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname);
 // 3x3 s1, fp16, LDS-DMA staging with counted vmcnt (conv_glds.hip)
 int launch_conv3x3_glds(const ConvArgs& a, int variant, hipStream_t s);
 
+// 3x3 s1, fp16, LDS-DMA with a deep weight ring, fully unrolled (conv_gx.h, conv_gx_l*.hip)
+int launch_conv3x3_gx_l2(const ConvArgs& a, int variant, hipStream_t s);
+int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s);
+int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s);
+
 // layer1 (Cin = Cout = 64), fp16: weight-resident persistent kernel (conv_c64.hip)
 int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s);
 

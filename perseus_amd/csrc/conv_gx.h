@@ -1,0 +1,361 @@
+// 3x3 stride-1 conv, fp16, LDS-DMA staging with a deep weight ring (the layer2-4
+// BasicBlock convs).  Same LDS images, MFMA roles and register epilogue as
+// conv_glds.hip, with three changes:
+//
+//  * prefetch distance PD: the weight tile of step s + PD is DMA'd at step s into
+//    a ring of PD + G slots (G = steps per barrier, below).  An L2-hit LDS-DMA under load takes about a
+//    microsecond to land (MI355X_MICROARCH.md, ldsdma-fill), i.e. several steps;
+//    distance 2-3 left every step waiting on it.
+//  * the K loop is unrolled completely, so every step's `s_waitcnt vmcnt(N)` is a
+//    compile-time count of the VMEM ops issued after the newest one the next
+//    step's fragment reads need (vm_after() below simulates the issue order).
+//  * XCD-aware block order (XG): the Cout/BN workgroups of one spatial tile get
+//    consecutive indices within one XCD's round-robin share (blocks b and b + 8
+//    share an XCD), so the halo patch they all read is an L2 hit after the first.
+//
+//  * G steps per barrier: the wait + s_barrier closes every G-th step only.
+//
+// Step s = (block cb = s / 9, tap = s % 9), one 64-channel K-slice of one tap,
+// two half-steps of 32 K.  Per step: read the fragments of half-step 2s+1, MFMAs
+// of 2s, read the fragments of 2s+2 (step s + 1); then the DMAs, in issue order
+// W(s + PD), at the first group start of a block the next block's patch, RSD steps before the end the bias
+// (+ residual) loads; MFMAs of 2s+1; wait for what step s + 2's fragments need and
+// cross a bare s_barrier.
+#pragma once
+#include <type_traits>
+
+#include "conv.h"
+
+namespace pa {
+
+typedef unsigned xu4 __attribute__((ext_vector_type(4)));
+
+template <int V>
+using xic = std::integral_constant<int, V>;
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void gx_for(F&& f) {
+  if constexpr (B < E) {
+    f(xic<B>{});
+    gx_for<B + 1, E>(f);
+  }
+}
+
+// 128 zero bytes (halo source); one copy per translation unit (no relocatable device code)
+static __device__ __attribute__((aligned(128))) unsigned gx_zero_line[32];
+
+__device__ __forceinline__ int xswz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int xfrag(int r) { return r < 4 ? 2 * r : (r < 12 ? 2 * (r - 4) + 1 : 2 * (r - 8)); }
+// weight row 16 t + 4 q + v of each 32-row group holds channel 8 q + 4 t + v: a
+// lane's tile pair covers 8 consecutive channels (16-byte epilogue accesses)
+__device__ __forceinline__ int xperm(int rho) {
+  return (rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);
+}
+
+template <int N>
+__device__ __forceinline__ void xwait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+#endif
+}
+// 16 B per lane global -> LDS (wave-uniform LDS base + lane * 16), as inline asm:
+// with the builtin, hipcc's waitcnt pass stops counting LDS reads in order once an
+// LDS-DMA is pending and waits lgkmcnt(0) at the next use of any LDS read (every
+// step, right after the barrier).  The pass does not see these VMEM ops, so every
+// wait for DMA'd data is the explicit xwait_vm; its own vmcnt waits (bias,
+// residual) only get more conservative.  M0 write -> LDS-DMA needs one wait state.
+__device__ __forceinline__ void xdma16(const void* src, char* lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const unsigned off = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in these kernels keeps it live
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(off), "v"(src) : "memory", "m0");
+#pragma clang diagnostic pop
+#endif
+}
+
+// Issue schedule (per wave), used at compile time.
+struct GxPlan {
+  int nsteps, ncb, pd, wdma, pdma, rl, rs, g;
+  int spb = 9;  // steps per 64-channel block (9 taps; conv_s2x.h adds the downsample)
+  // the patch of block c >= 1 is DMA'd at the first group start inside block c - 1
+  constexpr int ps(int c) const { return (spb * (c - 1) + g - 1) / g * g; }
+  constexpr int nw(int t) const { return t + pd < nsteps ? wdma : 0; }
+  constexpr int np(int t) const { return (t / spb + 1 < ncb && t == ps(t / spb + 1)) ? pdma : 0; }
+  constexpr int nr(int t) const { return t == rs ? rl : 0; }
+  constexpr int cum(int t) const {  // VMEM ops issued in steps 0..t (prologue excluded: it is drained)
+    int c = 0;
+    for (int u = 0; u <= t; ++u) c += nw(u) + np(u) + nr(u);
+    return c;
+  }
+  // ops issued after the newest op that the fragments of step v need
+  // (W(v), and the patch of block v / spb), counted at the end of step s
+  constexpr int vm_after(int s, int v) const {
+    int need = 0;  // issue position just past the newest needed op (0 = all in the prologue)
+    if (v >= pd) {
+      const int t = v - pd;
+      const int e = (t > 0 ? cum(t - 1) : 0) + nw(t);
+      need = e > need ? e : need;
+    }
+    const int cb = v / 9;
+    if (cb >= 1) {
+      const int t = ps(cb);
+      const int e = (t > 0 ? cum(t - 1) : 0) + nw(t) + np(t);
+      need = e > need ? e : need;
+    }
+    const int n = cum(s) - need;
+    return n < 0 ? 0 : (n > 63 ? 63 : n);
+  }
+};
+
+// DBG (timing experiments only, wrong results): 1 = no waits / barriers in the K loop,
+// 2 = also no weight / patch DMAs in the K loop
+template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0>
+__global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int NCB = CIN / 64;
+  constexpr int NSTEPS = NCB * 9;
+  constexpr int KTOT = 9 * CIN;
+  constexpr int PH = TH + 2, PW = TW + 2;
+  constexpr int IMS = (TW == 8) ? ((PH * PW + 7) / 16 * 16 + 8) : PH * PW;
+  constexpr int NP = NI * IMS;
+  constexpr int NPC = (NP * 8 + 63) / 64 * 64;
+  constexpr int PDMA = NPC / 64 / NW + (NPC / 64 % NW ? 1 : 0);
+  constexpr int PATCHB = (PDMA * NW * 64) * 16;
+  constexpr int WB = BN * 128;
+  constexpr int WDMA = BN * 8 / NT;
+  constexpr int BM = NI * TH * TW;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(BN * 8 % NT == 0 && WDMA >= 1, "weight tile / threads");
+  static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile");
+  static_assert(TW >= 16 || (TW == 8 && NI == 2), "fragment geometry");
+  static_assert(G >= 1 && G <= 3 && PD >= G + 1 && PD <= 8, "prefetch distance / steps per barrier");
+  // slot (t + PD) % NSLOT, written at step t, was last read by step t + PD - NSLOT,
+  // which must lie before the last barrier: t - G with a barrier every G steps
+  constexpr int NSLOT = PD + G;
+  constexpr int RL = TN + ((EPI & EPI_RES) ? TM * TN / 2 : 0);
+  // epilogue loads (bias, residual) issued RSD steps before the end: early enough to
+  // land, late enough not to hold their VGPRs across the whole K loop
+  constexpr int RSD = 4;
+  constexpr GxPlan plan{NSTEPS, NCB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G};
+  __shared__ __attribute__((aligned(1024))) char smem[2 * PATCHB + NSLOT * WB];
+  char* patch = smem;
+  char* wring = smem + 2 * PATCHB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int H = a.Hout, W = a.Wout;
+  const _Float16* __restrict__ in = (const _Float16*)a.in;
+  const _Float16* __restrict__ w = (const _Float16*)a.w;
+
+  const int Cout = a.Cout;
+  const int ntn = Cout / BN;
+  int tn_idx, sp;
+  if (xg) {
+    // b = 8 i + x (x: XCD share); i = ntn * j + tn  ->  spatial tile 8 j + x
+    const int b = blockIdx.x, x8 = b & 7, i = b >> 3;
+    tn_idx = i % ntn;
+    sp = (i / ntn) * 8 + x8;
+  } else {
+    tn_idx = blockIdx.x % ntn;
+    sp = blockIdx.x / ntn;
+  }
+  const int tw_n = W / TW, tpi = (H / TH) * tw_n;
+  const int img0 = (sp / tpi) * NI;
+  const int rem = sp - (sp / tpi) * tpi;
+  const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
+  const int n0 = tn_idx * BN;
+
+  const char* psrc[PDMA];
+#pragma unroll
+  for (int i = 0; i < PDMA; ++i) {
+    const int c = (i * NW + wid) * 64 + lane;
+    const int p = c >> 3, pc = c & 7;
+    const int lc = pc ^ ((p >> 1) & 7);
+    const int img = p / IMS, pp = p - (p / IMS) * IMS;
+    const int pr = pp / PW, pcl = pp - (pp / PW) * PW;
+    const int n = img0 + img, h = th0 + pr - 1, x = tw0 + pcl - 1;
+    const bool ok = p < NP && pr < PH && n < a.B && (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W;
+    psrc[i] = ok ? (const char*)(in + (((size_t)n * H + h) * W + x) * CIN + lc * 8) : nullptr;
+  }
+  auto dma_patch = [&](int cb, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PDMA; ++i) {
+      const char* s = psrc[i] ? psrc[i] + cb * 128 : (const char*)gx_zero_line;
+      xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
+    }
+  };
+  const _Float16* wsrc[WDMA];
+#pragma unroll
+  for (int i = 0; i < WDMA; ++i) {
+    const int c = (i * NW + wid) * 64 + lane;
+    const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
+    wsrc[i] = w + (size_t)(n0 + xperm(co)) * KTOT + lc * 8;
+  }
+  auto dma_w = [&](int s) __attribute__((always_inline)) {
+    const int cb = s / 9, tap = s % 9;
+#pragma unroll
+    for (int i = 0; i < WDMA; ++i)
+      xdma16(wsrc[i] + tap * CIN + cb * 64, wring + (s % NSLOT) * WB + (i * NW + wid) * 1024);
+  };
+
+  const int o = xfrag(r16);
+  int ppix[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int mb = wm * WTM + tm * 16;
+    if constexpr (TW == 8) {
+      ppix[tm] = (o >> 3) * IMS + (mb / 16) * PW + (o & 7);
+    } else {
+      ppix[tm] = (mb / (TH * TW)) * IMS + ((mb / TW) % TH) * PW + mb % TW + o;
+    }
+  }
+
+  const _Float16* __restrict__ res = (const _Float16*)a.res;
+  _Float16* __restrict__ out = (_Float16*)a.out;
+  size_t pixo[TM];
+  bool ok[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int mb = wm * WTM + tm * 16;
+    int img, y, x;
+    if constexpr (TW == 8) {
+      y = mb / 16;
+      img = o >> 3;
+      x = o & 7;
+    } else {
+      img = mb / (TH * TW);
+      y = (mb / TW) % TH;
+      x = mb % TW + o;
+    }
+    const int n = img0 + img;
+    ok[tm] = n < a.B;
+    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * Cout + n0 + wn * WTN + q * 8;
+  }
+  half8 rv[TM][TN / 2];
+  f32x4 bias[TN];
+  auto load_epi = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+      bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + n0 + wn * WTN + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4);
+    if constexpr (EPI & EPI_RES) {
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int p = 0; p < TN / 2; ++p) rv[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + p * 32);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: patch(0) and W(0 .. PD-1), drained
+  dma_patch(0, 0);
+#pragma unroll
+  for (int t = 0; t < PD; ++t)
+    if (t < NSTEPS) dma_w(t);
+  xwait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+
+  // fragments one half-step (32 of the 64 K of a step) ahead: sub-step k = 2 S + g
+  // reads into set k & 1 while the MFMAs of sub-step k - 1 run
+  xu4 fa[2][TN], fb[2][TM];
+  auto read_frags = [&](auto kc) __attribute__((always_inline)) {
+    constexpr int K = decltype(kc)::value;
+    constexpr int S = K >> 1, HG = K & 1, CB = S / 9, TAP = S % 9;
+    constexpr int TOFF = (TAP / 3) * PW + (TAP % 3);
+    const char* pb = patch + (CB & 1) * PATCHB;
+    const char* wb = wring + (S % NSLOT) * WB;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+      fa[HG][tn] = *reinterpret_cast<const xu4*>(wb + xswz(wn * WTN + tn * 16 + r16, HG * 4 + q));
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) fb[HG][tm] = *reinterpret_cast<const xu4*>(pb + xswz(ppix[tm] + TOFF, HG * 4 + q));
+  };
+  auto mfma = [&](auto gc) __attribute__((always_inline)) {
+    constexpr int HG = decltype(gc)::value;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[HG][tn]),
+                                                             __builtin_bit_cast(half8, fb[HG][tm]), acc[tm][tn], 0, 0, 0);
+  };
+  read_frags(xic<0>{});
+  gx_for<0, NSTEPS>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int S = decltype(sc)::value;
+    constexpr int CB = S / 9, TAP = S % 9;
+    read_frags(xic<2 * S + 1>{});
+    __builtin_amdgcn_s_setprio(1);
+    mfma(xic<0>{});
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (S + 1 < NSTEPS) read_frags(xic<2 * S + 2>{});
+    // DMAs after this step's LDS reads (they are issued by then; see xdma16)
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (S + PD < NSTEPS && DBG < 2) dma_w(S + PD);
+    if constexpr (CB + 1 < NCB && S == plan.ps(CB + 1) && DBG < 2) dma_patch(CB + 1, (CB + 1) & 1);
+    if constexpr (S == plan.rs) {
+      // vm_after() counts these after this step's DMAs: keep the scheduler from
+      // moving the (read-only) loads across them
+      __builtin_amdgcn_sched_barrier(0);
+      load_epi();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma(xic<1>{});
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS && DBG == 0) {
+      // the next group (steps s+1 .. s+G) reads the fragments of steps up to s+G+1
+      // (first half): those weight tiles and their blocks' patches must have landed
+      constexpr int V = S + G + 1 < NSTEPS ? S + G + 1 : NSTEPS - 1;
+      xwait_vm<plan.vm_after(S, V)>();
+      __builtin_amdgcn_s_barrier();
+    }
+  });
+  xwait_vm<0>();  // bias / residual (also waited for by the compiler at their use)
+
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    if (!ok[tm]) continue;
+#pragma unroll
+    for (int p = 0; p < TN / 2; ++p) {
+      half8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = acc[tm][2 * p + (j >> 2)][j & 3] + bias[2 * p + (j >> 2)][j & 3];
+        if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
+        hv[j] = (_Float16)fmaxf(v, 0.f);
+      }
+      *reinterpret_cast<half8*>(out + pixo[tm] + p * 32) = hv;
+    }
+  }
+}
+
+template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0>
+static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
+  PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "gx conv: epilogue %d", a.epi);
+  PA_CHECK(a.Cin == CIN, "gx conv: Cin %d != %d", a.Cin, CIN);
+  PA_CHECK(a.Hout % TH == 0 && a.Wout % TW == 0, "gx conv: %dx%d not tiled by %dx%d", a.Hout, a.Wout, TH, TW);
+  PA_CHECK(a.Cout % BN == 0, "gx conv: Cout %d %% BN %d", a.Cout, BN);
+  const int ntn = a.Cout / BN;
+  const int nsp = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW);
+  const int tiles = nsp * ntn;
+  const int x = xg && nsp % 8 == 0;  // whole groups of 8 spatial tiles only
+  if (a.epi & EPI_RES)
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG>), dim3(tiles),
+                       dim3(WM * WN * 64), 0, s, a, x);
+  else
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG>), dim3(tiles), dim3(WM * WN * 64), 0, s,
+                       a, x);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+}  // namespace pa

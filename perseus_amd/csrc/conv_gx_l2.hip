@@ -1,0 +1,17 @@
+// conv_gx.h instantiations for layer2 (32x32, 128 channels) (one file per layer: the fully unrolled
+// kernels compile in parallel).  variant & 3 selects the tile / prefetch distance,
+// variant & 4 turns the XCD-aware block order off.
+#include "conv_gx.h"
+
+namespace pa {
+
+int launch_conv3x3_gx_l2(const ConvArgs& a, int variant, hipStream_t s) {
+  if (a.B <= 0) return PA_OK;
+  const bool xg = !(variant & 4);
+  switch (variant & 3) {
+      case 1: return run_gx<16, 16, 1, 64, 4, 2, 128, 6>(a, xg, s);
+      default: return run_gx<16, 16, 1, 128, 4, 2, 128, 3>(a, xg, s);
+  }
+}
+
+}  // namespace pa

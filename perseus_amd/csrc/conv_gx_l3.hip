@@ -1,0 +1,19 @@
+// conv_gx.h instantiations for layer3 (16x16, 256 channels) (one file per layer: the fully unrolled
+// kernels compile in parallel).  variant & 3 selects the tile / prefetch distance,
+// variant & 4 turns the XCD-aware block order off.
+#include "conv_gx.h"
+
+namespace pa {
+
+int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s) {
+  if (a.B <= 0) return PA_OK;
+  const bool xg = !(variant & 4);
+  switch (variant & 3) {
+      case 1: return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 2>(a, xg, s);
+      case 2: return run_gx<16, 16, 1, 64, 4, 2, 256, 4, 3>(a, xg, s);
+      case 3: return run_gx<16, 16, 1, 64, 4, 1, 256, 3, 2>(a, xg, s);
+      default: return run_gx<16, 16, 1, 64, 4, 2, 256, 3>(a, xg, s);
+  }
+}
+
+}  // namespace pa

@@ -418,11 +418,17 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
   }
   if constexpr (std::is_same<T, _Float16>::value) {
     const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : 4;
-    // layers 2-4: LDS-DMA kernel (measured 5-13 % under the register-staged one);
-    // shipped configs: layer2 plain, layers 3/4 with the fragment prefetch
-    const int gv = g_variant[layer] >= 40 && g_variant[layer] <= 43 ? g_variant[layer] - 40
-                   : g_variant[layer] == 0 && layer >= 2                ? (layer == 2 ? 0 : 2)
-                                                                         : -1;
+    // layers 2-4: conv_gx (deep-ring LDS-DMA, inline-asm DMA, fully unrolled);
+    // variants 50-57 pick its alternatives, 40-43 the older conv_glds kernel
+    if (layer >= 2 && (g_variant[layer] == 0 || (g_variant[layer] >= 50 && g_variant[layer] <= 57))) {
+      static const char* names[5] = {"", "conv3x3x_l1", "conv3x3x_l2", "conv3x3x_l3", "conv3x3x_l4"};
+      if (kname) *kname = names[layer];
+      const int v = g_variant[layer] == 0 ? 0 : g_variant[layer] - 50;
+      if (a.Cin == 128 && a.Hout == 32) return launch_conv3x3_gx_l2(a, v, s);
+      if (a.Cin == 256 && a.Hout == 16) return launch_conv3x3_gx_l3(a, v, s);
+      if (a.Cin == 512 && a.Hout == 8) return launch_conv3x3_gx_l4(a, v, s);
+    }
+    const int gv = g_variant[layer] >= 40 && g_variant[layer] <= 43 ? g_variant[layer] - 40 : -1;
     if (gv >= 0) {
       static const char* names[5] = {"", "conv3x3g_l1", "conv3x3g_l2", "conv3x3g_l3", "conv3x3g_l4"};
       if (kname) *kname = names[layer];

@@ -1,0 +1,245 @@
+// Stride-2 BasicBlock entry on conv_gx.h's machinery, fp16: conv 3x3 s2 (+ bn1,
+// relu) and the 1x1 s2 downsample (+ bn) in one pass over the input
+// (torchvision resnet18 layer2/3/4 block 0; replaces
+// conv_s2.hip / conv_s2p.hip on the fp16 path).
+//
+// The downsample reads input pixel (2y, 2x), the centre tap of the 3x3 window of
+// output (y, x): per 64-channel input block the K loop has 10 steps, the 9 taps
+// into `acc` and the downsample slice (its 1x1 weights against the centre tap's
+// patch pixels) into `accd`.  Every step is a conv_gx step: weight tile DMA'd
+// PD steps ahead into a ring, fragments read half a step ahead, compile-time
+// vmcnt plan (GxPlan with 10 steps per block), a bare s_barrier every G steps.
+//
+// Patch: (2TH + 1) input rows x (2TW + 1) columns, stored de-interleaved (the TW + 1
+// even input columns, then the TW odd ones) so that for every tap 16 consecutive
+// output columns read 16 consecutive LDS positions; out-of-image pixels read a
+// zero line.  Output pixels are row-major over the TH x TW tile (16-pixel MFMA
+// fragment = one row at TW = 16, two rows at TW = 8; for TW = 8 the row pitch is
+// padded to 20 positions so the two rows of a fragment fall on disjoint banks).
+#pragma once
+#include "conv_gx.h"
+
+namespace pa {
+
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G>
+__global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int NCB = CIN / 64;
+  constexpr int SPB = 10;  // 9 taps + downsample per 64-channel block
+  constexpr int NSTEPS = NCB * SPB;
+  constexpr int KTOT = 9 * CIN;
+  constexpr int PH = 2 * TH + 1;
+  constexpr int PW = TW == 8 ? 20 : 2 * TW + 1;  // LDS positions per patch row
+  constexpr int NP = PH * PW;
+  constexpr int NPC = (NP * 8 + 63) / 64 * 64;
+  constexpr int PDMA = NPC / 64 / NW + (NPC / 64 % NW ? 1 : 0);
+  constexpr int PATCHB = (PDMA * NW * 64) * 16;
+  constexpr int NPB = NCB > 1 ? 2 : 1;  // patch buffers
+  constexpr int WB = BN * 128;
+  constexpr int WDMA = BN * 8 / NT;
+  constexpr int BM = TH * TW;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(TW == 8 || TW == 16, "tile width");
+  static_assert(BN * 8 % NT == 0 && WDMA >= 1, "weight tile / threads");
+  static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile");
+  static_assert(G >= 1 && G <= 3 && PD >= G + 1 && PD <= 8, "prefetch distance / steps per barrier");
+  constexpr int NSLOT = PD + G;
+  constexpr int RL = 2 * TN;  // epilogue loads: bias, bias2
+  constexpr int RSD = 4;
+  constexpr GxPlan plan{NSTEPS, NCB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, SPB};
+  __shared__ __attribute__((aligned(1024))) char smem[NPB * PATCHB + NSLOT * WB];
+  char* patch = smem;
+  char* wring = smem + NPB * PATCHB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int H = a.Hout, W = a.Wout, Hin = a.Hin, Win = a.Win, Cout = a.Cout;
+  const _Float16* __restrict__ in = (const _Float16*)a.in;
+  const _Float16* __restrict__ w = (const _Float16*)a.w;
+  const _Float16* __restrict__ wds = (const _Float16*)a.wds;
+
+  const int ntn = Cout / BN;
+  int tn_idx, sp;
+  if (xg) {  // blocks b and b + 8 share an XCD: the N-tiles of one spatial tile there
+    const int b = blockIdx.x, x8 = b & 7, i = b >> 3;
+    tn_idx = i % ntn;
+    sp = (i / ntn) * 8 + x8;
+  } else {
+    tn_idx = blockIdx.x % ntn;
+    sp = blockIdx.x / ntn;
+  }
+  const int tw_n = W / TW, tpi = (H / TH) * tw_n;
+  const int img = sp / tpi;
+  const int rem = sp - img * tpi;
+  const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
+  const int n0 = tn_idx * BN;
+
+  // patch DMA: LDS slot c = (i * NW + wid) * 64 + lane holds position p = c >> 3,
+  // logical chunk (c & 7) ^ swizzle(p)
+  const char* psrc[PDMA];
+#pragma unroll
+  for (int i = 0; i < PDMA; ++i) {
+    const int c = (i * NW + wid) * 64 + lane;
+    const int p = c >> 3, pc = c & 7;
+    const int lc = pc ^ ((p >> 1) & 7);
+    const int pr = p / PW, pos = p - (p / PW) * PW;
+    const int col = pos <= TW ? 2 * pos : 2 * (pos - TW - 1) + 1;
+    const int h = 2 * th0 - 1 + pr, x = 2 * tw0 - 1 + col;
+    const bool ok = p < NP && pos < 2 * TW + 1 && img < a.B && (unsigned)h < (unsigned)Hin && (unsigned)x < (unsigned)Win;
+    psrc[i] = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * CIN + lc * 8) : nullptr;
+  }
+  auto dma_patch = [&](int cb, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PDMA; ++i) {
+      const char* s = psrc[i] ? psrc[i] + cb * 128 : (const char*)gx_zero_line;
+      xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
+    }
+  };
+  // weights: ring row co holds output channel n0 + xperm(co) (16-byte epilogue)
+  const _Float16* wsrc[WDMA];
+  const _Float16* dsrc[WDMA];
+#pragma unroll
+  for (int i = 0; i < WDMA; ++i) {
+    const int c = (i * NW + wid) * 64 + lane;
+    const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
+    wsrc[i] = w + (size_t)(n0 + xperm(co)) * KTOT + lc * 8;
+    dsrc[i] = wds + (size_t)(n0 + xperm(co)) * CIN + lc * 8;
+  }
+  auto dma_w = [&](int s) __attribute__((always_inline)) {
+    const int cb = s / SPB, t = s % SPB;
+#pragma unroll
+    for (int i = 0; i < WDMA; ++i) {
+      const _Float16* src = t < 9 ? wsrc[i] + t * CIN + cb * 64 : dsrc[i] + cb * 64;
+      xdma16(src, wring + (s % NSLOT) * WB + (i * NW + wid) * 1024);
+    }
+  };
+
+  const int o = xfrag(r16);
+  int ppix[TM];  // LDS position of tap (0, 0) for this lane's pixel of fragment tm
+  size_t pixo[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int m = wm * WTM + tm * 16 + o;
+    const int y = m / TW, x = m - (m / TW) * TW;
+    ppix[tm] = 2 * y * PW + x;
+    pixo[tm] = (((size_t)(img < a.B ? img : 0) * H + th0 + y) * W + tw0 + x) * Cout + n0 + wn * WTN + q * 8;
+  }
+  f32x4 bias[TN], bias2[TN];
+  auto load_epi = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int c = n0 + wn * WTN + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4;
+      bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + c);
+      bias2[tn] = *reinterpret_cast<const f32x4*>(a.bias2 + c);
+    }
+  };
+
+  f32x4 acc[TM][TN], accd[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      accd[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  dma_patch(0, 0);
+#pragma unroll
+  for (int t = 0; t < PD; ++t)
+    if (t < NSTEPS) dma_w(t);
+  xwait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+
+  xu4 fa[2][TN], fb[2][TM];
+  auto read_frags = [&](auto kc) __attribute__((always_inline)) {
+    constexpr int K = decltype(kc)::value;
+    constexpr int S = K >> 1, HG = K & 1, CB = S / SPB, T = S % SPB;
+    constexpr int TT = T < 9 ? T : 4;  // the downsample reads the centre tap's pixels
+    constexpr int KX = TT % 3;
+    constexpr int TOFF = (TT / 3) * PW + (KX == 0 ? 0 : (KX == 1 ? TW + 1 : 1));
+    const char* pb = patch + (NPB == 2 ? (CB & 1) : 0) * PATCHB;
+    const char* wb = wring + (S % NSLOT) * WB;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+      fa[HG][tn] = *reinterpret_cast<const xu4*>(wb + xswz(wn * WTN + tn * 16 + r16, HG * 4 + q));
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) fb[HG][tm] = *reinterpret_cast<const xu4*>(pb + xswz(ppix[tm] + TOFF, HG * 4 + q));
+  };
+  auto mfma = [&](auto hc, auto dsc) __attribute__((always_inline)) {
+    constexpr int HG = decltype(hc)::value;
+    constexpr bool DS = decltype(dsc)::value;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        f32x4& d = DS ? accd[tm][tn] : acc[tm][tn];
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[HG][tn]),
+                                                   __builtin_bit_cast(half8, fb[HG][tm]), d, 0, 0, 0);
+      }
+  };
+  read_frags(xic<0>{});
+  gx_for<0, NSTEPS>([&](auto sc) __attribute__((always_inline)) {
+    constexpr int S = decltype(sc)::value;
+    constexpr int CB = S / SPB;
+    using DS = std::integral_constant<bool, S % SPB == 9>;
+    read_frags(xic<2 * S + 1>{});
+    __builtin_amdgcn_s_setprio(1);
+    mfma(xic<0>{}, DS{});
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (S + 1 < NSTEPS) read_frags(xic<2 * S + 2>{});
+    // DMAs after this step's LDS reads (see xdma16); order = GxPlan's
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (S + PD < NSTEPS) dma_w(S + PD);
+    if constexpr (CB + 1 < NCB && S == plan.ps(CB + 1)) dma_patch(CB + 1, (CB + 1) & 1);
+    if constexpr (S == plan.rs) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_epi();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma(xic<1>{}, DS{});
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS) {
+      constexpr int V = S + G + 1 < NSTEPS ? S + G + 1 : NSTEPS - 1;
+      xwait_vm<plan.vm_after(S, V)>();
+      __builtin_amdgcn_s_barrier();
+    }
+  });
+  xwait_vm<0>();
+
+  if (img >= a.B) return;
+  _Float16* __restrict__ out = (_Float16*)a.out;
+  _Float16* __restrict__ out2 = (_Float16*)a.out2;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int p = 0; p < TN / 2; ++p) {
+      half8 h1, h2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tn = 2 * p + (j >> 2), e = j & 3;
+        h1[j] = (_Float16)fmaxf(acc[tm][tn][e] + bias[tn][e], 0.f);
+        h2[j] = (_Float16)(accd[tm][tn][e] + bias2[tn][e]);
+      }
+      *reinterpret_cast<half8*>(out + pixo[tm] + p * 32) = h1;
+      *reinterpret_cast<half8*>(out2 + pixo[tm] + p * 32) = h2;
+    }
+}
+
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1>
+static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
+  PA_CHECK(a.Cin == CIN, "s2x conv: Cin %d != %d", a.Cin, CIN);
+  PA_CHECK(a.Hin == 2 * a.Hout && a.Win == 2 * a.Wout, "s2x conv: %dx%d -> %dx%d", a.Hin, a.Win, a.Hout, a.Wout);
+  PA_CHECK(a.Hout % TH == 0 && a.Wout % TW == 0, "s2x conv: %dx%d not tiled by %dx%d", a.Hout, a.Wout, TH, TW);
+  PA_CHECK(a.Cout % BN == 0, "s2x conv: Cout %d %% BN %d", a.Cout, BN);
+  const int ntn = a.Cout / BN;
+  const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW);
+  const int x = xg && nsp % 8 == 0;
+  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G>), dim3(nsp * ntn), dim3(WM * WN * 64), 0, s, a, x);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+}  // namespace pa
