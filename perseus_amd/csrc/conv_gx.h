@@ -99,7 +99,7 @@ struct GxPlan {
       const int e = (t > 0 ? cum(t - 1) : 0) + nw(t);
       need = e > need ? e : need;
     }
-    const int cb = v / 9;
+    const int cb = v / spb;
     if (cb >= 1) {
       const int t = ps(cb);
       const int e = (t > 0 ? cum(t - 1) : 0) + nw(t) + np(t);

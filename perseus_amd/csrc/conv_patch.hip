@@ -435,7 +435,11 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       return launch_conv3x3_glds(a, gv, s);
     }
     // layer1: the weight-resident persistent kernel for all four convs (variant 32
-    // keeps the patch kernel for reference timing)
+    // keeps the patch kernel for reference timing; 33 = conv_l1x)
+    if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && g_variant[1] == 33) {
+      if (kname) *kname = "conv3x3l1x_l1";
+      return launch_conv3x3_l1x(a, s);
+    }
     const bool c64 = g_variant[1] == 30 || g_variant[1] == 31 || g_variant[1] == 0;
     if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && c64) {
       if (kname) *kname = "conv3x3c64_l1";

@@ -48,6 +48,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   constexpr int RL = 2 * TN;  // epilogue loads: bias, bias2
   constexpr int RSD = 4;
   constexpr GxPlan plan{NSTEPS, NCB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, SPB};
+  static_assert(NPB * PATCHB + NSLOT * WB <= 163840, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[NPB * PATCHB + NSLOT * WB];
   char* patch = smem;
   char* wring = smem + NPB * PATCHB;
