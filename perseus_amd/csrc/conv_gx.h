@@ -112,7 +112,8 @@ struct GxPlan {
 
 // DBG (timing experiments only, wrong results): 1 = no waits / barriers in the K loop,
 // 2 = also no weight / patch DMAs in the K loop
-template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0>
+// FD: fragment reads run FD half-steps ahead of the MFMAs (FD + 1 register sets)
+template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
@@ -265,38 +266,44 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   __builtin_amdgcn_s_barrier();
 
   // fragments one half-step (32 of the 64 K of a step) ahead: sub-step k = 2 S + g
-  // reads into set k & 1 while the MFMAs of sub-step k - 1 run
-  xu4 fa[2][TN], fb[2][TM];
+  // reads into set k % (FD + 1) while the MFMAs of an earlier sub-step run
+  static_assert(FD == 1 || FD == 2, "fragment distance");
+  constexpr int NSET = FD + 1;
+  xu4 fa[NSET][TN], fb[NSET][TM];
   auto read_frags = [&](auto kc) __attribute__((always_inline)) {
     constexpr int K = decltype(kc)::value;
-    constexpr int S = K >> 1, HG = K & 1, CB = S / 9, TAP = S % 9;
+    constexpr int S = K >> 1, HG = K & 1, CB = S / 9, TAP = S % 9, SET = K % NSET;
     constexpr int TOFF = (TAP / 3) * PW + (TAP % 3);
     const char* pb = patch + (CB & 1) * PATCHB;
     const char* wb = wring + (S % NSLOT) * WB;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
-      fa[HG][tn] = *reinterpret_cast<const xu4*>(wb + xswz(wn * WTN + tn * 16 + r16, HG * 4 + q));
+      fa[SET][tn] = *reinterpret_cast<const xu4*>(wb + xswz(wn * WTN + tn * 16 + r16, HG * 4 + q));
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm) fb[HG][tm] = *reinterpret_cast<const xu4*>(pb + xswz(ppix[tm] + TOFF, HG * 4 + q));
+    for (int tm = 0; tm < TM; ++tm) fb[SET][tm] = *reinterpret_cast<const xu4*>(pb + xswz(ppix[tm] + TOFF, HG * 4 + q));
   };
-  auto mfma = [&](auto gc) __attribute__((always_inline)) {
-    constexpr int HG = decltype(gc)::value;
+  auto mfma = [&](auto kc) __attribute__((always_inline)) {
+    constexpr int SET = decltype(kc)::value % NSET;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
-        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[HG][tn]),
-                                                             __builtin_bit_cast(half8, fb[HG][tm]), acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[SET][tn]),
+                                                             __builtin_bit_cast(half8, fb[SET][tm]), acc[tm][tn], 0, 0, 0);
   };
+  // step s + 1's data landed before the barrier that closed step s - 1, so with
+  // FD = 2 both its halves are read during step s
   read_frags(xic<0>{});
+  if constexpr (FD == 2) read_frags(xic<1>{});
   gx_for<0, NSTEPS>([&](auto sc) __attribute__((always_inline)) {
     constexpr int S = decltype(sc)::value;
     constexpr int CB = S / 9, TAP = S % 9;
-    read_frags(xic<2 * S + 1>{});
+    if constexpr (FD == 1) read_frags(xic<2 * S + 1>{});
+    else if constexpr (S + 1 < NSTEPS) read_frags(xic<2 * S + 2>{});
     __builtin_amdgcn_s_setprio(1);
-    mfma(xic<0>{});
+    mfma(xic<2 * S>{});
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (S + 1 < NSTEPS) read_frags(xic<2 * S + 2>{});
+    if constexpr (S + 1 < NSTEPS) read_frags(xic<2 * S + 1 + FD>{});
     // DMAs after this step's LDS reads (they are issued by then; see xdma16)
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + PD < NSTEPS && DBG < 2) dma_w(S + PD);
@@ -309,7 +316,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    mfma(xic<1>{});
+    mfma(xic<2 * S + 1>{});
     __builtin_amdgcn_s_setprio(0);
     if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS && DBG == 0) {
       // the next group (steps s+1 .. s+G) reads the fragments of steps up to s+G+1
@@ -338,7 +345,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   }
 }
 
-template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0>
+template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1>
 static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "gx conv: epilogue %d", a.epi);
   PA_CHECK(a.Cin == CIN, "gx conv: Cin %d != %d", a.Cin, CIN);
@@ -349,10 +356,10 @@ static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
   const int tiles = nsp * ntn;
   const int x = xg && nsp % 8 == 0;  // whole groups of 8 spatial tiles only
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG>), dim3(tiles),
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD>), dim3(tiles),
                        dim3(WM * WN * 64), 0, s, a, x);
   else
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG>), dim3(tiles), dim3(WM * WN * 64), 0, s,
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD>), dim3(tiles), dim3(WM * WN * 64), 0, s,
                        a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;

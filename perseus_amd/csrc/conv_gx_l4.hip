@@ -11,7 +11,7 @@ int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s) {
   switch (variant & 3) {
       case 1: return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 2>(a, xg, s);
       case 2: return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 3>(a, xg, s);
-      case 3: return run_gx<8, 8, 2, 64, 2, 2, 512, 4, 2>(a, xg, s);
+      case 3: return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 0, 2>(a, xg, s);
       default: return run_gx<8, 8, 2, 64, 4, 2, 512, 4>(a, xg, s);
   }
 }

@@ -28,6 +28,20 @@ from . import _lib
 from .synth import float_keys, resnet18_shapes
 
 
+# Bumped whenever any module registers (or re-assigns) a parameter or buffer, so a
+# model's cached tensor list for the weight fingerprint is rebuilt after structural
+# changes; in-place updates (load_state_dict copies) show in each tensor's _version.
+_REG_EPOCH = [0]
+
+
+def _bump_epoch(*_args, **_kw):
+    _REG_EPOCH[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump_epoch)
+torch.nn.modules.module.register_module_buffer_registration_hook(_bump_epoch)
+
+
 class _Conv(nn.Module):
     def __init__(self, shape):
         super().__init__()
@@ -100,7 +114,12 @@ class KeypointCNN(nn.Module):
 
     # -------------------------------------------------------------- weights
     def _fingerprint(self):
-        return tuple((t._version, t.data_ptr()) for t in self.state_dict(keep_vars=True).values())
+        # state_dict() walks the module tree (~130 us per forward); the tensor list is
+        # cached until a parameter/buffer registration anywhere bumps _REG_EPOCH
+        if getattr(self, "_fp_epoch", None) != _REG_EPOCH[0]:
+            self._fp_tensors = list(self.state_dict(keep_vars=True).values())
+            self._fp_epoch = _REG_EPOCH[0]
+        return tuple((t._version, t.data_ptr()) for t in self._fp_tensors)
 
     def _blob(self) -> np.ndarray:
         sd = self.state_dict()

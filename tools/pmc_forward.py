@@ -20,12 +20,17 @@ def main():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--precision", default="fp16")
     p.add_argument("--out", required=True)
+    p.add_argument("--variant", action="append", default=[], help="LAYER:VARIANT (pa_debug_set_variant)")
     a = p.parse_args()
     import numpy as np
     import torch
 
-    from perseus_amd import synth
+    from perseus_amd import _lib, synth
     from perseus_amd.detector import KeypointCNN
+
+    for lv in a.variant:
+        layer, v = (int(t) for t in lv.split(":"))
+        _lib.check(_lib.lib().pa_debug_set_variant(layer, v))
 
     dev = torch.device("cuda", 0)
     m = KeypointCNN(num_channels=4, precision=a.precision)
