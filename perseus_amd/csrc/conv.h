@@ -39,9 +39,6 @@ int launch_conv3x3s2_ds_p(const ConvS2Args& a, int variant, hipStream_t s);
 // fp16, LDS-DMA deep ring (conv_s2x.h, conv_s2x_l.hip), layers 2-4
 int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
 
-// layer1 (Cin = Cout = 64), fp16: weight-resident persistent kernel v2 (conv_l1x.hip)
-int launch_conv3x3_l1x(const ConvArgs& a, hipStream_t s);
-
 template <typename T>
 int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);
 

@@ -111,7 +111,7 @@ struct GxPlan {
 };
 
 // DBG (timing experiments only, wrong results): 1 = no waits / barriers in the K loop,
-// 2 = also no weight / patch DMAs in the K loop
+// 2 = also no weight / patch DMAs in the K loop, 3 = no K loop (prologue + epilogue)
 // FD: fragment reads run FD half-steps ahead of the MFMAs (FD + 1 register sets)
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   // FD = 2 both its halves are read during step s
   read_frags(xic<0>{});
   if constexpr (FD == 2) read_frags(xic<1>{});
-  gx_for<0, NSTEPS>([&](auto sc) __attribute__((always_inline)) {
+  gx_for<0, (DBG == 3 ? 0 : NSTEPS)>([&](auto sc) __attribute__((always_inline)) {
     constexpr int S = decltype(sc)::value;
     constexpr int CB = S / 9, TAP = S % 9;
     if constexpr (FD == 1) read_frags(xic<2 * S + 1>{});
@@ -326,6 +326,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
       __builtin_amdgcn_s_barrier();
     }
   });
+  if constexpr (DBG == 3) load_epi();
   xwait_vm<0>();  // bias / residual (also waited for by the compiler at their use)
 
 #pragma unroll

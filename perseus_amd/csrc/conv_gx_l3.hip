@@ -8,8 +8,10 @@ namespace pa {
 int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s) {
   if (a.B <= 0) return PA_OK;
   const bool xg = !(variant & 4);
+  if (variant == 8) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 2>(a, xg, s);  // timing only
+  if (variant == 9) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 3>(a, xg, s);  // timing only
   switch (variant & 3) {
-      case 1: return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 2>(a, xg, s);
+      case 1: return run_gx<8, 16, 1, 64, 2, 2, 256, 3>(a, xg, s);  // 80 KB LDS: 2 workgroups per CU
       case 2: return run_gx<16, 16, 1, 64, 4, 2, 256, 4, 3>(a, xg, s);
       case 3: return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 0, 2>(a, xg, s);
       default: return run_gx<16, 16, 1, 64, 4, 2, 256, 3>(a, xg, s);

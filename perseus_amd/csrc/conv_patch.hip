@@ -420,7 +420,7 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
     const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : 4;
     // layers 2-4: conv_gx (deep-ring LDS-DMA, inline-asm DMA, fully unrolled);
     // variants 50-57 pick its alternatives, 40-43 the older conv_glds kernel
-    if (layer >= 2 && (g_variant[layer] == 0 || (g_variant[layer] >= 50 && g_variant[layer] <= 57))) {
+    if (layer >= 2 && (g_variant[layer] == 0 || (g_variant[layer] >= 50 && g_variant[layer] <= 59))) {
       static const char* names[5] = {"", "conv3x3x_l1", "conv3x3x_l2", "conv3x3x_l3", "conv3x3x_l4"};
       if (kname) *kname = names[layer];
       const int v = g_variant[layer] == 0 ? 0 : g_variant[layer] - 50;
@@ -435,11 +435,7 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       return launch_conv3x3_glds(a, gv, s);
     }
     // layer1: the weight-resident persistent kernel for all four convs (variant 32
-    // keeps the patch kernel for reference timing; 33 = conv_l1x)
-    if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && g_variant[1] == 33) {
-      if (kname) *kname = "conv3x3l1x_l1";
-      return launch_conv3x3_l1x(a, s);
-    }
+    // keeps the patch kernel for reference timing)
     const bool c64 = g_variant[1] == 30 || g_variant[1] == 31 || g_variant[1] == 0;
     if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && c64) {
       if (kname) *kname = "conv3x3c64_l1";
