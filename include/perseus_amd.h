@@ -86,6 +86,10 @@ int pa_detector_time_launch(pa_detector* d, const float* x_dev, int B, float* y_
                             int reps, float* avg_ms_out, const char** name_out);
 
 int pa_debug_set_variant(int layer, int variant);
+/* Timestamping kernel variants write s_memrealtime stamps (100 MHz) to
+ * trace_dev + launch * 65536 + workgroup * 64 (launch = index in the forward, stem = 0);
+ * nullptr turns it off.  Measurement entry point. */
+int pa_debug_set_trace(unsigned long long* trace_dev);
 
 /* Algorithmic FLOPs of one frame's forward (2 x MAC over the 20 convs + fc). */
 double pa_detector_flops_per_frame(const pa_detector* d);

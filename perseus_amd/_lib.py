@@ -51,6 +51,7 @@ _SIGS = {
     "pa_detector_time_launch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                           C.c_int, C.c_void_p, C.c_void_p]),
     "pa_debug_set_variant": (C.c_int, [C.c_int, C.c_int]),
+    "pa_debug_set_trace": (C.c_int, [C.c_void_p]),
     "pa_preprocess_rgbd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.c_float, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "pa_keypoints_postprocess": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,

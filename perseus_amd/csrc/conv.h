@@ -8,6 +8,15 @@ namespace pa {
 enum { EPI_RELU = 1, EPI_RES = 2 };
 
 extern int g_variant[8];  // kernel-variant selector per layer (A/B timing; 0 = shipped)
+// pa_debug_set_trace: device buffer for the timestamping variants; launch i of a
+// forward gets g_trace + i * TRACE_LAUNCH (nullptr = off)
+extern unsigned long long* g_trace;
+constexpr int TRACE_SLOTS = 64, TRACE_LAUNCH = 65536;
+
+// one s_memrealtime stamp per workgroup (thread 0) into slot `slot`
+__device__ __forceinline__ void trace_stamp(unsigned long long* tr, int slot) {
+  if (threadIdx.x == 0 && slot < TRACE_SLOTS) tr[blockIdx.x * TRACE_SLOTS + slot] = __builtin_amdgcn_s_memrealtime();
+}
 
 struct ConvArgs {
   const void* in;     // NHWC [B][Hin][Win][Cin]
@@ -16,6 +25,7 @@ struct ConvArgs {
   const void* res;    // NHWC [B][Hout][Wout][Cout] or nullptr
   void* out;          // NHWC [B][Hout][Wout][Cout]
   int B, Hin, Win, Cin, Hout, Wout, Cout, stride, pad, epi, M;
+  unsigned long long* trace;  // timing-only variants: s_memrealtime stamps, TRACE_SLOTS per workgroup
 };
 
 // conv3x3 s2 (+bn, relu) -> out and 1x1 s2 downsample (+bn) -> out2, one pass
@@ -28,6 +38,7 @@ struct ConvS2Args {
   void* out;           // NHWC [B][Hout][Wout][Cout]
   void* out2;          // NHWC [B][Hout][Wout][Cout]
   int B, Hin, Win, Cin, Hout, Wout, Cout;
+  unsigned long long* trace;  // as ConvArgs::trace
 };
 
 template <typename T>
@@ -55,6 +66,8 @@ int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s);
 
 // layer1 (Cin = Cout = 64), fp16: weight-resident persistent kernel (conv_c64.hip)
 int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s);
+// the same with LDS-DMA staging spread through the K loop (conv_c64d.hip)
+int launch_conv3x3_c64d(const ConvArgs& a, int variant, hipStream_t s);
 
 template <typename T>
 int launch_conv3x3_pipe(const ConvArgs& a, int variant, hipStream_t s);

@@ -8,6 +8,8 @@
 //   B[k][co] = W'[co][kr][ks][c]  (BatchNorm folded on the host),
 // k ordered (kr, ks, c) so that one K-step = one filter tap x 128 bytes of
 // channels = one contiguous 128-byte NHWC segment per output pixel.
+#include <type_traits>
+
 #include "conv.h"
 
 namespace pa {
@@ -504,7 +506,7 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ in, int
   }
   for (int j = 0; j < nout; ++j) {
     float v = 0.f;
-    if (c < C) v = fcw[(size_t)j * C + c] * m0 + fcw[(size_t)j * C + c + 1] * m1;
+    if (c < C) v = fmaf(fcw[(size_t)j * C + c + 1], m1, fcw[(size_t)j * C + c] * m0);  // explicit: head_fp16 matches
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if (lane == 0) part[wid][j] = v;
@@ -513,11 +515,64 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ in, int
   if (tid < nout) y[(size_t)n * nout + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + fcb[tid];
 }
 
+// fp16, HW = 64, C = 512 (the 256x256 forward): head_kernel's arithmetic in the same
+// order, with every load (16 pixels per thread, the thread's fc weights) issued
+// before the first add.  head_kernel's runtime-length fc loop waits for each
+// output's weights in turn (~10 us per batch-64 launch).
+template <int NOUT>
+__global__ __launch_bounds__(256) void head_fp16(const _Float16* __restrict__ in, const float* __restrict__ fcw,
+                                                 const float* __restrict__ fcb, float* __restrict__ y) {
+  constexpr int HW = 64, C = 512;
+  __shared__ float csum[4][C];
+  __shared__ float part[4][NOUT];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = tid >> 6, c8 = tid & 63;  // pixel group, 16-B channel chunk
+  const _Float16* p = in + (size_t)n * HW * C + c8 * 8;
+  half8 h[HW / 4];
+#pragma unroll
+  for (int u = 0; u < HW / 4; ++u) h[u] = *reinterpret_cast<const half8*>(p + (size_t)(g + 4 * u) * C);
+  const int c = 2 * tid;
+  float fw[NOUT][2];
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    const float2 v = *reinterpret_cast<const float2*>(fcw + (size_t)j * C + c);
+    fw[j][0] = v.x;
+    fw[j][1] = v.y;
+  }
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < HW / 4; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += (float)h[u][e];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) csum[g][c8 * 8 + e] = s[e];
+  __syncthreads();
+  const float inv = 1.0f / (float)HW;
+  const float m0 = (csum[0][c] + csum[1][c] + csum[2][c] + csum[3][c]) * inv;
+  const float m1 = (csum[0][c + 1] + csum[1][c + 1] + csum[2][c + 1] + csum[3][c + 1]) * inv;
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    float v = fmaf(fw[j][1], m1, fw[j][0] * m0);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) part[wid][j] = v;
+  }
+  __syncthreads();
+  if (tid < NOUT) y[(size_t)n * NOUT + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + fcb[tid];
+}
+
 template <typename T>
 int launch_head(const T* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
                 hipStream_t s) {
   PA_CHECK(C == 512 && nout <= 32, "head: C=%d nout=%d", C, nout);  // 4 pixel groups x 64 chunks
   if (B <= 0) return PA_OK;
+  if constexpr (std::is_same<T, _Float16>::value) {
+    if (HW == 64 && nout == 16 && g_variant[7] == 0) {
+      hipLaunchKernelGGL(head_fp16<16>, dim3(B), dim3(256), 0, s, in, fcw, fcb, y);
+      PA_LAUNCH_CHECK();
+      return PA_OK;
+    }
+  }
   hipLaunchKernelGGL(head_kernel<T>, dim3(B), dim3(256), 0, s, in, HW, C, fcw, fcb, nout, y);
   PA_LAUNCH_CHECK();
   return PA_OK;

@@ -52,7 +52,10 @@ __device__ __forceinline__ int c64perm(int rho) {
   return (rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);
 }
 
-template <int WM, int EPI>
+// DBG (timing-only variants, wrong results): 1 = no MFMA loop, 2 = no next-patch
+// loads (every tile reuses the first patch), 3 = no weight staging; 4 = the
+// shipped kernel plus s_memrealtime stamps into a.trace (conv.h trace_stamp)
+template <int WM, int EPI, int DBG = 0>
 __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
   using namespace c64;
   constexpr int NT = WM * 64;
@@ -71,9 +74,10 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
   const _Float16* __restrict__ in = (const _Float16*)a.in;
   const _Float16* __restrict__ w = (const _Float16*)a.w;
   const int tw_n = W / TW, tpi = (H / TH) * tw_n;
+  if constexpr (DBG == 4) trace_stamp(a.trace, 0);
 
   // ---- weights -> LDS once: row = tap * 64 + co, source [co][tap][64 ch]
-  {
+  if constexpr (DBG != 3) {
     constexpr int HALF = (WCH + 1) / 2;  // two batches to bound live registers
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -135,11 +139,13 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
   load_patch(tile);
   store_patch(0);
   __syncthreads();
+  if constexpr (DBG == 4) trace_stamp(a.trace, 1);
 
   for (int t = 0; tile < ntiles; ++t, tile += gridDim.x) {
     const int buf = t & 1;
     const int next = tile + gridDim.x;
-    load_patch(next);  // zeros past the last tile (never read)
+    if constexpr (DBG != 2) load_patch(next);  // zeros past the last tile (never read)
+    if constexpr (DBG == 4) trace_stamp(a.trace, 2 + 4 * t);
 
     const int img = tile / tpi, rem = tile - (tile / tpi) * tpi;
     const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
@@ -191,12 +197,14 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
                                                                __builtin_bit_cast(half8, fb[S][tm]), acc[tm][tn], 0,
                                                                0, 0);
     };
+    if constexpr (DBG != 1) {
     rd(c64ic<0>{});
     static_for<0, 18>([&](auto kc) __attribute__((always_inline)) {
       constexpr int K = decltype(kc)::value;
       if constexpr (K + 1 < 18) rd(c64ic<K + 1>{});
       mm(kc);
     });
+    }
 
     _Float16* __restrict__ out = (_Float16*)a.out;
 #pragma unroll
@@ -213,11 +221,18 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
         }
         *reinterpret_cast<half8*>(out + pixo[tm] + p * 32 + q * 8) = hv;
       }
+    if constexpr (DBG == 4) trace_stamp(a.trace, 3 + 4 * t);
 
     // next tile's patch into the other buffer (last read during tile t-1, before
     // the previous barrier), then one barrier
-    store_patch(buf ^ 1);
+    if constexpr (DBG != 2) store_patch(buf ^ 1);
+    if constexpr (DBG == 4) trace_stamp(a.trace, 4 + 4 * t);
     __syncthreads();
+    if constexpr (DBG == 4) trace_stamp(a.trace, 5 + 4 * t);
+  }
+  if constexpr (DBG == 4) {
+    __builtin_amdgcn_s_waitcnt(0);
+    trace_stamp(a.trace, 63);
   }
 }
 
@@ -232,14 +247,14 @@ static int num_cus() {
   return n;
 }
 
-template <int WM>
+template <int WM, int DBG = 0>
 static int run_c64(const ConvArgs& a, hipStream_t s) {
   const int tiles = a.B * (a.Hout / c64::TH) * (a.Wout / c64::TW);
   const int grid = tiles < num_cus() ? tiles : num_cus();
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_c64<WM, EPI_RELU | EPI_RES>), dim3(grid), dim3(WM * 64), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64<WM, EPI_RELU | EPI_RES, DBG>), dim3(grid), dim3(WM * 64), 0, s, a, tiles);
   else
-    hipLaunchKernelGGL((conv3x3_c64<WM, EPI_RELU>), dim3(grid), dim3(WM * 64), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64<WM, EPI_RELU, DBG>), dim3(grid), dim3(WM * 64), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -250,7 +265,14 @@ int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s) {
   PA_CHECK(a.Hout % c64::TH == 0 && a.Wout % c64::TW == 0, "c64 conv: %dx%d not tiled by 16x16", a.Hout, a.Wout);
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "c64 conv: epilogue %d", a.epi);
   if (a.B <= 0) return PA_OK;
-  return variant == 1 ? run_c64<4>(a, s) : run_c64<8>(a, s);
+  switch (variant) {
+    case 1: return run_c64<4>(a, s);
+    case 7: return run_c64<8, 1>(a, s);
+    case 8: return run_c64<8, 2>(a, s);
+    case 9: return run_c64<8, 3>(a, s);
+    case 6: return a.trace ? run_c64<8, 4>(a, s) : run_c64<8>(a, s);
+    default: return run_c64<8>(a, s);
+  }
 }
 
 }  // namespace pa

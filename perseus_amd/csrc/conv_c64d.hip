@@ -1,0 +1,242 @@
+// Layer1 3x3 stride-1 conv (Cin = Cout = 64), fp16: conv_c64.hip's weight-resident
+// persistent kernel with its staging moved onto LDS-DMA (conv_gx.h's inline-asm
+// global_load_lds_dwordx4 and explicit vmcnt waits).
+//
+// conv_c64.hip loads the next tile's 18 x 18 x 64 halo patch into registers at the
+// start of a tile (48 KB per CU issued in one burst), then writes it to LDS after
+// the MFMAs; timestamps (tools/trace_launch.py) show ~0.6 us per tile in that
+// issue burst and the LDS store, outside the MFMA stream.  Here the patch of tile
+// t + 1 is DMA'd straight into the idle patch buffer, one wave-instruction every
+// other (tap, 32-channel) group of tile t, so the loads overlap the MFMAs and
+// nothing is staged through VGPRs.  The weights (9 taps x 64 rows, one DMA per tap
+// per lane) and the first patch are DMA'd in the prologue.
+//
+// LDS: 72 KB weights (row = tap * 64 + permuted output channel) + 2 x 41 KB patch
+// buffers (324 patch pixels rounded up to 41 wave-DMAs of 64 x 16 B), the same
+// 128-byte swizzled rows, lane -> pixel map and channel-pair permutation as
+// conv_gx.h, so the epilogue is c64's.
+#include "conv_gx.h"
+
+namespace pa {
+
+namespace c64d {
+constexpr int TH = 16, TW = 16, PH = TH + 2, PW = TW + 2, NP = PH * PW;  // 324 patch pixels
+constexpr int NWAVE = 8, NT = NWAVE * 64;
+constexpr int PJ = (NP * 8 + 63) / 64;  // 41 patch wave-DMAs
+constexpr int PATCHB = PJ * 1024;
+constexpr int WBYTES = 9 * 64 * 128;  // 73,728
+static_assert(PJ == 5 * NWAVE + 1, "patch DMA split: 5 per wave + 1 on wave 0");
+static_assert(WBYTES + 2 * PATCHB <= 160 * 1024, "LDS");
+}  // namespace c64d
+
+// DBG: 4 = s_memrealtime stamps into a.trace (as conv_c64.hip)
+template <int EPI, int DBG = 0>
+__global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
+  using namespace c64d;
+  constexpr int WTM = TH * TW / NWAVE;  // 32 pixels per wave
+  constexpr int TM = WTM / 16, TN = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[WBYTES + 2 * PATCHB];
+  char* wl = smem;
+  char* patch = smem + WBYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int H = a.Hout, W = a.Wout;
+  const _Float16* __restrict__ in = (const _Float16*)a.in;
+  const _Float16* __restrict__ w = (const _Float16*)a.w;
+  const int tw_n = W / TW, tpi = (H / TH) * tw_n;
+  if constexpr (DBG == 4) trace_stamp(a.trace, 0);
+
+  // this lane's patch chunks: DMA i of wave wid covers chunk (i * 8 + wid) * 64 + lane
+  // (i = 5 only on wave 0); pixel p = chunk >> 3, logical chunk = physical ^ swizzle
+  int prow[6], pcol[6], pch[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int c = ((i < 5 ? i * NWAVE + wid : 5 * NWAVE)) * 64 + lane;
+    const int p = c >> 3;
+    prow[i] = p < NP ? p / PW : 1 << 20;  // rows past the patch: always out of range
+    pcol[i] = p - (p / PW) * PW;
+    pch[i] = ((c & 7) ^ ((p >> 1) & 7)) * 8;
+  }
+  auto dma_patch = [&](int i, int tile, int buf) __attribute__((always_inline)) {
+    const int img = tile / tpi, rem = tile - img * tpi;
+    const int h = (rem / tw_n) * TH + prow[i] - 1, x = (rem - (rem / tw_n) * tw_n) * TW + pcol[i] - 1;
+    const void* src = ((unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W)
+                          ? (const void*)(in + (((size_t)img * H + h) * W + x) * 64 + pch[i])
+                          : (const void*)gx_zero_line;
+    xdma16(src, patch + buf * PATCHB + (i < 5 ? i * NWAVE + wid : 5 * NWAVE) * 1024);
+  };
+
+  const int o = xfrag(r16);
+  int ppix[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int mb = wid * WTM + tm * 16;
+    ppix[tm] = (mb / TW) * PW + mb % TW + o;
+  }
+  // bias before the DMAs, so that no compiler-visible load sits between them and the
+  // per-tap waits of the first tile below
+  f32x4 bias[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // prologue: patch of the first tile, then the 9 weight taps (tap i = DMA i of
+  // every wave); the first tile waits for each tap just before it reads it
+  int tile = blockIdx.x;
+  if (wid == 0) dma_patch(5, tile, 0);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) dma_patch(i, tile, 0);
+  {
+    const int row0 = wid * 8 + (lane >> 3);  // row within the tap
+    const int lc = (lane & 7) ^ ((row0 >> 1) & 7);
+    const _Float16* src = w + (size_t)xperm(row0) * 576 + lc * 8;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) xdma16(src + i * 64, wl + (i * NWAVE + wid) * 1024);
+  }
+  xwait_vm<8>();  // patch + tap 0
+  lds_barrier();
+  if constexpr (DBG == 4) trace_stamp(a.trace, 1);
+
+  for (int t = 0; tile < ntiles; ++t, tile += gridDim.x) {
+    const int buf = t & 1;
+    const int next = tile + gridDim.x;
+    const bool has_next = next < ntiles;
+    const int img = tile / tpi, rem = tile - img * tpi;
+    const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
+    size_t pixo[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int mb = wid * WTM + tm * 16;
+      pixo[tm] = (((size_t)img * H + th0 + mb / TW) * W + tw0 + mb % TW + o) * 64 + q * 8;
+    }
+    half8 rv[TM][TN / 2];
+    if constexpr (EPI & EPI_RES) {
+      const _Float16* __restrict__ res = (const _Float16*)a.res;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int p = 0; p < TN / 2; ++p) rv[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + p * 32);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (DBG == 4) trace_stamp(a.trace, 2 + 4 * t);
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* pb = patch + buf * PATCHB;
+    xu4 fa[2][TN], fb[2][TM];
+    auto rd = [&](auto kc) __attribute__((always_inline)) {
+      constexpr int K = decltype(kc)::value, TAP = K >> 1, HG = K & 1, S = K & 1;
+      constexpr int TOFF = (TAP / 3) * PW + (TAP % 3);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        fa[S][tn] = *reinterpret_cast<const xu4*>(wl + xswz(TAP * 64 + tn * 16 + r16, HG * 4 + q));
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) fb[S][tm] = *reinterpret_cast<const xu4*>(pb + xswz(ppix[tm] + TOFF, HG * 4 + q));
+    };
+    auto mm = [&](auto kc) __attribute__((always_inline)) {
+      constexpr int S = decltype(kc)::value & 1;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[S][tn]),
+                                                               __builtin_bit_cast(half8, fb[S][tm]), acc[tm][tn], 0, 0, 0);
+    };
+    rd(xic<0>{});
+    gx_for<0, 18>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int K = decltype(kc)::value;
+      if constexpr (K % 2 == 1 && K + 1 < 18) {
+        // first tile: tap (K + 1) / 2's weights.  VMEM ops issued after that DMA:
+        // the later taps, the residual loads, and this tile's patch DMAs so far (odd
+        // groups < K; wave 0's extra one at group 0 only makes its wait stricter)
+        constexpr int TAPN = (K + 1) / 2;
+        constexpr int R = (EPI & EPI_RES) ? TM * TN / 2 : 0;
+        constexpr int J = (K - 1) / 2 < 5 ? (K - 1) / 2 : 5;
+        if (t == 0) {
+          if (has_next)
+            xwait_vm<8 - TAPN + R + J>();
+          else
+            xwait_vm<8 - TAPN + R>();
+          lds_barrier();
+        }
+      }
+      if constexpr (K + 1 < 18) rd(xic<K + 1>{});
+      // next tile's patch: wave 0's extra DMA at group 0, then one per odd group
+      if constexpr (K == 0 || (K % 2 == 1 && K / 2 < 5)) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (has_next) {
+          if constexpr (K == 0) {
+            if (wid == 0) dma_patch(5, next, buf ^ 1);
+          } else {
+            dma_patch(K / 2, next, buf ^ 1);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mm(kc);
+    });
+    xwait_vm<0>();  // next patch (+ residual)
+
+    _Float16* __restrict__ out = (_Float16*)a.out;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int p = 0; p < TN / 2; ++p) {
+        half8 hv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v = acc[tm][2 * p + (j >> 2)][j & 3] + bias[2 * p + (j >> 2)][j & 3];
+          if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
+          hv[j] = (_Float16)fmaxf(v, 0.f);
+        }
+        *reinterpret_cast<half8*>(out + pixo[tm] + p * 32) = hv;
+      }
+    if constexpr (DBG == 4) trace_stamp(a.trace, 3 + 4 * t);
+    // every wave's DMAs into buf ^ 1 landed (its wait above) and its reads of buf
+    // retired (the MFMAs consumed them): one barrier hands both buffers over
+    lds_barrier();
+    if constexpr (DBG == 4) trace_stamp(a.trace, 5 + 4 * t);
+  }
+  if constexpr (DBG == 4) {
+    __builtin_amdgcn_s_waitcnt(0);
+    trace_stamp(a.trace, 63);
+  }
+}
+
+static int num_cus_d() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int DBG>
+static int run_c64d(const ConvArgs& a, hipStream_t s) {
+  const int tiles = a.B * (a.Hout / c64d::TH) * (a.Wout / c64d::TW);
+  const int grid = tiles < num_cus_d() ? tiles : num_cus_d();
+  if (a.epi & EPI_RES)
+    hipLaunchKernelGGL((conv3x3_c64d<EPI_RELU | EPI_RES, DBG>), dim3(grid), dim3(512), 0, s, a, tiles);
+  else
+    hipLaunchKernelGGL((conv3x3_c64d<EPI_RELU, DBG>), dim3(grid), dim3(512), 0, s, a, tiles);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+int launch_conv3x3_c64d(const ConvArgs& a, int variant, hipStream_t s) {
+  PA_CHECK(a.Cin == 64 && a.Cout == 64 && a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout,
+           "c64d conv: Cin=Cout=64 stride-1 only");
+  PA_CHECK(a.Hout % c64d::TH == 0 && a.Wout % c64d::TW == 0, "c64d conv: %dx%d not tiled by 16x16", a.Hout, a.Wout);
+  PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "c64d conv: epilogue %d", a.epi);
+  if (a.B <= 0) return PA_OK;
+  return variant == 4 && a.trace ? run_c64d<4>(a, s) : run_c64d<0>(a, s);
+}
+
+}  // namespace pa

@@ -402,6 +402,7 @@ static int run_patch(const ConvArgs& a, hipStream_t s) {
 // Stride-1 3x3 conv, Hin == Hout.  Tile configuration per feature-map size;
 // g_variant[layer] (pa_debug_set_variant) selects alternatives for A/B timing.
 int g_variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+unsigned long long* g_trace = nullptr;
 
 template <typename T>
 int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
@@ -436,10 +437,21 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
     }
     // layer1: the weight-resident persistent kernel for all four convs (variant 32
     // keeps the patch kernel for reference timing)
-    const bool c64 = g_variant[1] == 30 || g_variant[1] == 31 || g_variant[1] == 0;
-    if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && c64) {
+    // shipped: the residual convs on the LDS-DMA variant (25.5 vs 28.5 us), the
+    // others on the register-staged one (24.3 vs 24.8 us)
+    const bool l1 = a.Hout == 64 && a.Cout == 64 && a.Cin == 64;
+    if (l1 && g_variant[1] == 0) {
       if (kname) *kname = "conv3x3c64_l1";
-      return launch_conv3x3_c64(a, g_variant[1] == 31 ? 1 : 0, s);
+      return (a.epi & EPI_RES) ? launch_conv3x3_c64d(a, 0, s) : launch_conv3x3_c64(a, 0, s);
+    }
+    const bool c64 = g_variant[1] >= 30 && g_variant[1] <= 39 && g_variant[1] != 32;
+    if (l1 && c64) {
+      if (kname) *kname = "conv3x3c64_l1";
+      return launch_conv3x3_c64(a, g_variant[1] - 30, s);
+    }
+    if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && g_variant[1] >= 60 && g_variant[1] <= 69) {
+      if (kname) *kname = "conv3x3c64_l1";
+      return launch_conv3x3_c64d(a, g_variant[1] - 60, s);
     }
   }
   if (a.Hout == 64 && a.Cout == 64) {

@@ -251,6 +251,8 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     PA_RUN(launch_maxpool<T>(S, B, 128, 128, 64, X, s), "maxpool");
   }
   int hw = 64;
+  int launch = 1;  // stem = 0
+  auto trace = [&]() { return g_trace ? g_trace + (size_t)TRACE_LAUNCH * launch++ : nullptr; };
   for (const Block& b : d->blocks) {
     const ConvL& c1 = d->convs[b.conv1];
     const ConvL& c2 = d->convs[b.conv2];
@@ -283,6 +285,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       sa.Hout = ho;
       sa.Wout = ho;
       sa.Cout = c1.cout;
+      sa.trace = trace();
       PA_RUN(launch_conv3x3s2_ds<T>(sa, s, &kn), kn);
       res = D;
       out = D;
@@ -298,6 +301,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       a.stride = c1.stride;
       a.pad = 1;
       a.epi = EPI_RELU;
+      a.trace = trace();
       if (c1.stride == 1)
         PA_RUN(launch_conv3x3_s1<T>(a, s, &kn), kn);
       else
@@ -333,6 +337,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     b2.stride = 1;
     b2.pad = 1;
     b2.epi = EPI_RELU | EPI_RES;
+    b2.trace = trace();
     PA_RUN(launch_conv3x3_s1<T>(b2, s, &kn), kn);
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
@@ -473,6 +478,11 @@ int pa_detector_time_launch(pa_detector* d, const float* x_dev, int B, float* y_
   hipEventDestroy(p.t0);
   hipEventDestroy(p.t1);
   return rc;
+}
+
+int pa_debug_set_trace(unsigned long long* trace_dev) {
+  pa::g_trace = trace_dev;
+  return PA_OK;
 }
 
 int pa_debug_set_variant(int layer, int variant) {

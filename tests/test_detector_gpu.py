@@ -158,11 +158,17 @@ def test_kernel_variants_agree_bit_for_bit(B):
     m = model(0)
     x = torch.from_numpy(synth.synthetic_frames(2, B)).cuda()
     y0 = m(x)
-    try:
-        for layer, variant in ((1, 3), (2, 1), (3, 1), (4, 1), (6, 3), (0, 10)):
-            _lib.check(L.pa_debug_set_variant(layer, variant))
-        y1 = m(x)
-    finally:
-        for layer in range(8):
-            L.pa_debug_set_variant(layer, 0)
-    assert torch.equal(y0, y1)
+    sets = (
+        ((1, 3), (2, 1), (3, 1), (4, 1), (6, 3), (0, 10)),
+        ((1, 30), (7, 1)),  # layer1: register-staged kernel on every conv; the generic head
+        ((1, 60),),  # layer1: LDS-DMA kernel on every conv
+    )
+    for vs in sets:
+        try:
+            for layer, variant in vs:
+                _lib.check(L.pa_debug_set_variant(layer, variant))
+            y1 = m(x)
+        finally:
+            for layer in range(8):
+                L.pa_debug_set_variant(layer, 0)
+        assert torch.equal(y0, y1), vs
