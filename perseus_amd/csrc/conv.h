@@ -6,12 +6,26 @@
 namespace pa {
 
 enum { EPI_RELU = 1, EPI_RES = 2 };
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 extern int g_variant[8];  // kernel-variant selector per layer (A/B timing; 0 = shipped)
 // pa_debug_set_trace: device buffer for the timestamping variants; launch i of a
 // forward gets g_trace + i * TRACE_LAUNCH (nullptr = off)
 extern unsigned long long* g_trace;
 constexpr int TRACE_SLOTS = 64, TRACE_LAUNCH = 65536;
+
+// 16-byte store at byte offset `off` from the wave-uniform base `base`; WT = write-through
+// (sc1: the line goes on to memory now instead of sitting dirty in this XCD's L2
+// until the end-of-kernel write-back)
+template <bool WT>
+__device__ __forceinline__ void store16(void* base, unsigned off, half8 v) {
+  if constexpr (WT) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)off, 0, 16);
+  } else {
+    *reinterpret_cast<half8*>((char*)base + off) = v;
+  }
+}
 
 // one s_memrealtime stamp per workgroup (thread 0) into slot `slot`
 __device__ __forceinline__ void trace_stamp(unsigned long long* tr, int slot) {

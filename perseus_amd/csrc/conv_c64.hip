@@ -55,7 +55,7 @@ __device__ __forceinline__ int c64perm(int rho) {
 // DBG (timing-only variants, wrong results): 1 = no MFMA loop, 2 = no next-patch
 // loads (every tile reuses the first patch), 3 = no weight staging; 4 = the
 // shipped kernel plus s_memrealtime stamps into a.trace (conv.h trace_stamp)
-template <int WM, int EPI, int DBG = 0>
+template <int WM, int EPI, int DBG = 0, bool WT = false>
 __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
   using namespace c64;
   constexpr int NT = WM * 64;
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(WM * 64) void conv3x3_c64(ConvArgs a, int ntiles) {
           v = fmaxf(v, 0.f);
           hv[j] = (_Float16)v;
         }
-        *reinterpret_cast<half8*>(out + pixo[tm] + p * 32 + q * 8) = hv;
+        store16<WT>(out, (unsigned)((pixo[tm] + p * 32 + q * 8) * 2), hv);
       }
     if constexpr (DBG == 4) trace_stamp(a.trace, 3 + 4 * t);
 
@@ -247,14 +247,15 @@ static int num_cus() {
   return n;
 }
 
-template <int WM, int DBG = 0>
+template <int WM, int DBG = 0, bool WT = false>
 static int run_c64(const ConvArgs& a, hipStream_t s) {
+  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * 64 * 2 < 0x7fffffffu, "c64 conv: output over 2 GB");
   const int tiles = a.B * (a.Hout / c64::TH) * (a.Wout / c64::TW);
   const int grid = tiles < num_cus() ? tiles : num_cus();
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_c64<WM, EPI_RELU | EPI_RES, DBG>), dim3(grid), dim3(WM * 64), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64<WM, EPI_RELU | EPI_RES, DBG, WT>), dim3(grid), dim3(WM * 64), 0, s, a, tiles);
   else
-    hipLaunchKernelGGL((conv3x3_c64<WM, EPI_RELU, DBG>), dim3(grid), dim3(WM * 64), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64<WM, EPI_RELU, DBG, WT>), dim3(grid), dim3(WM * 64), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -267,11 +268,12 @@ int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s) {
   if (a.B <= 0) return PA_OK;
   switch (variant) {
     case 1: return run_c64<4>(a, s);
+    case 5: return run_c64<8, 0, false>(a, s);  // plain (write-back) stores
     case 7: return run_c64<8, 1>(a, s);
     case 8: return run_c64<8, 2>(a, s);
     case 9: return run_c64<8, 3>(a, s);
     case 6: return a.trace ? run_c64<8, 4>(a, s) : run_c64<8>(a, s);
-    default: return run_c64<8>(a, s);
+    default: return run_c64<8, 0, true>(a, s);
   }
 }
 

@@ -30,7 +30,7 @@ static_assert(WBYTES + 2 * PATCHB <= 160 * 1024, "LDS");
 }  // namespace c64d
 
 // DBG: 4 = s_memrealtime stamps into a.trace (as conv_c64.hip)
-template <int EPI, int DBG = 0>
+template <int EPI, int DBG = 0, bool WT = false>
 __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
   using namespace c64d;
   constexpr int WTM = TH * TW / NWAVE;  // 32 pixels per wave
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
           if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
           hv[j] = (_Float16)fmaxf(v, 0.f);
         }
-        *reinterpret_cast<half8*>(out + pixo[tm] + p * 32) = hv;
+        store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), hv);
       }
     if constexpr (DBG == 4) trace_stamp(a.trace, 3 + 4 * t);
     // every wave's DMAs into buf ^ 1 landed (its wait above) and its reads of buf
@@ -218,14 +218,15 @@ static int num_cus_d() {
   return n;
 }
 
-template <int DBG>
+template <int DBG, bool WT = false>
 static int run_c64d(const ConvArgs& a, hipStream_t s) {
+  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * 64 * 2 < 0x7fffffffu, "c64d conv: output over 2 GB");
   const int tiles = a.B * (a.Hout / c64d::TH) * (a.Wout / c64d::TW);
   const int grid = tiles < num_cus_d() ? tiles : num_cus_d();
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_c64d<EPI_RELU | EPI_RES, DBG>), dim3(grid), dim3(512), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64d<EPI_RELU | EPI_RES, DBG, WT>), dim3(grid), dim3(512), 0, s, a, tiles);
   else
-    hipLaunchKernelGGL((conv3x3_c64d<EPI_RELU, DBG>), dim3(grid), dim3(512), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64d<EPI_RELU, DBG, WT>), dim3(grid), dim3(512), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -236,7 +237,8 @@ int launch_conv3x3_c64d(const ConvArgs& a, int variant, hipStream_t s) {
   PA_CHECK(a.Hout % c64d::TH == 0 && a.Wout % c64d::TW == 0, "c64d conv: %dx%d not tiled by 16x16", a.Hout, a.Wout);
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "c64d conv: epilogue %d", a.epi);
   if (a.B <= 0) return PA_OK;
-  return variant == 4 && a.trace ? run_c64d<4>(a, s) : run_c64d<0>(a, s);
+  if (variant == 4 && a.trace) return run_c64d<4>(a, s);
+  return variant == 2 ? run_c64d<0, false>(a, s) : run_c64d<0, true>(a, s);  // 2: plain (write-back) stores
 }
 
 }  // namespace pa

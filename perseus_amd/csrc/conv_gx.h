@@ -111,9 +111,11 @@ struct GxPlan {
 };
 
 // DBG (timing experiments only, wrong results): 1 = no waits / barriers in the K loop,
-// 2 = also no weight / patch DMAs in the K loop, 3 = no K loop (prologue + epilogue)
+// 2 = also no weight / patch DMAs in the K loop, 3 = no K loop (prologue + epilogue);
+// 4 = the shipped kernel plus s_memrealtime stamps into a.trace (conv.h trace_stamp)
 // FD: fragment reads run FD half-steps ahead of the MFMAs (FD + 1 register sets)
-template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1>
+template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1,
+          bool WT = true>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
@@ -165,6 +167,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     tn_idx = blockIdx.x % ntn;
     sp = blockIdx.x / ntn;
   }
+  if constexpr (DBG == 4) trace_stamp(a.trace, 0);
   const int tw_n = W / TW, tpi = (H / TH) * tw_n;
   const int img0 = (sp / tpi) * NI;
   const int rem = sp - (sp / tpi) * tpi;
@@ -264,6 +267,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     if (t < NSTEPS) dma_w(t);
   xwait_vm<0>();
   __builtin_amdgcn_s_barrier();
+  if constexpr (DBG == 4) trace_stamp(a.trace, 1);
 
   // fragments one half-step (32 of the 64 K of a step) ahead: sub-step k = 2 S + g
   // reads into set k % (FD + 1) while the MFMAs of an earlier sub-step run
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     __builtin_amdgcn_s_setprio(1);
     mfma(xic<2 * S + 1>{});
     __builtin_amdgcn_s_setprio(0);
-    if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS && DBG == 0) {
+    if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS && (DBG == 0 || DBG == 4)) {
       // the next group (steps s+1 .. s+G) reads the fragments of steps up to s+G+1
       // (first half): those weight tiles and their blocks' patches must have landed
       constexpr int V = S + G + 1 < NSTEPS ? S + G + 1 : NSTEPS - 1;
@@ -327,6 +331,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     }
   });
   if constexpr (DBG == 3) load_epi();
+  if constexpr (DBG == 4) trace_stamp(a.trace, 2);
   xwait_vm<0>();  // bias / residual (also waited for by the compiler at their use)
 
 #pragma unroll
@@ -341,12 +346,18 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
         if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
         hv[j] = (_Float16)fmaxf(v, 0.f);
       }
-      *reinterpret_cast<half8*>(out + pixo[tm] + p * 32) = hv;
+      store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), hv);
     }
+  }
+  if constexpr (DBG == 4) {
+    trace_stamp(a.trace, 3);
+    __builtin_amdgcn_s_waitcnt(0);
+    trace_stamp(a.trace, 63);
   }
 }
 
-template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1>
+template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1,
+          bool WT = true>
 static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "gx conv: epilogue %d", a.epi);
   PA_CHECK(a.Cin == CIN, "gx conv: Cin %d != %d", a.Cin, CIN);
@@ -356,11 +367,12 @@ static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
   const int nsp = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW);
   const int tiles = nsp * ntn;
   const int x = xg && nsp % 8 == 0;  // whole groups of 8 spatial tiles only
+  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 < 0x7fffffffu, "gx conv: output over 2 GB");
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD>), dim3(tiles),
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT>), dim3(tiles),
                        dim3(WM * WN * 64), 0, s, a, x);
   else
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD>), dim3(tiles), dim3(WM * WN * 64), 0, s,
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT>), dim3(tiles), dim3(WM * WN * 64), 0, s,
                        a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;

@@ -8,6 +8,8 @@ namespace pa {
 int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s) {
   if (a.B <= 0) return PA_OK;
   const bool xg = !(variant & 4);
+  if (variant == 6) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 0, 1, false>(a, true, s);  // plain (write-back) stores
+  if (variant == 7 && a.trace) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 4>(a, true, s);  // timestamps
   if (variant == 8) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 2>(a, xg, s);  // timing only
   if (variant == 9) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 3>(a, xg, s);  // timing only
   switch (variant & 3) {

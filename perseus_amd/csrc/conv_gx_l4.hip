@@ -8,6 +8,8 @@ namespace pa {
 int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s) {
   if (a.B <= 0) return PA_OK;
   const bool xg = !(variant & 4);
+  if (variant == 6) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 0, 1, false>(a, true, s);  // plain (write-back) stores
+  if (variant == 7 && a.trace) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 4>(a, true, s);  // timestamps
   switch (variant & 3) {
       case 1: return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 2>(a, xg, s);
       case 2: return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 3>(a, xg, s);

@@ -21,7 +21,7 @@
 
 namespace pa {
 
-template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G>
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G, bool WT = true>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
@@ -224,13 +224,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
         h1[j] = (_Float16)fmaxf(acc[tm][tn][e] + bias[tn][e], 0.f);
         h2[j] = (_Float16)(accd[tm][tn][e] + bias2[tn][e]);
       }
-      *reinterpret_cast<half8*>(out + pixo[tm] + p * 32) = h1;
-      *reinterpret_cast<half8*>(out2 + pixo[tm] + p * 32) = h2;
+      store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), h1);
+      store16<WT>(out2, (unsigned)((pixo[tm] + p * 32) * 2), h2);
     }
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1>
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1, bool WT = true>
 static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
+  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 < 0x7fffffffu, "s2x conv: output over 2 GB");
   PA_CHECK(a.Cin == CIN, "s2x conv: Cin %d != %d", a.Cin, CIN);
   PA_CHECK(a.Hin == 2 * a.Hout && a.Win == 2 * a.Wout, "s2x conv: %dx%d -> %dx%d", a.Hin, a.Win, a.Hout, a.Wout);
   PA_CHECK(a.Hout % TH == 0 && a.Wout % TW == 0, "s2x conv: %dx%d not tiled by %dx%d", a.Hout, a.Wout, TH, TW);
@@ -238,7 +239,7 @@ static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
   const int ntn = a.Cout / BN;
   const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW);
   const int x = xg && nsp % 8 == 0;
-  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G>), dim3(nsp * ntn), dim3(WM * WN * 64), 0, s, a, x);
+  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT>), dim3(nsp * ntn), dim3(WM * WN * 64), 0, s, a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -394,7 +394,7 @@ __global__ __launch_bounds__(512) void stem_pool2_fp16(const float* __restrict__
 // (all 7 kh x 64 channels, 112 VGPRs per lane) is loaded once, so the MFMA phase
 // reads only the input fragments from LDS.  One LDS-only barrier per pair; waves
 // 0-3 do MFMAs then pooling, waves 4-7 the other order (SIMD partners overlap).
-template <int PBT, int D>
+template <int PBT, int D, bool WT = false>
 __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__ x, int B, int Cin,
                                                        const _Float16* __restrict__ w, const float* __restrict__ bias,
                                                        _Float16* __restrict__ out) {
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__
         half8 m = *reinterpret_cast<const half8*>(vr + crow_swz(2 * qc, c8));
         m = __builtin_elementwise_max(m, *reinterpret_cast<const half8*>(vr + crow_swz(2 * qc + 1, c8)));
         if (qc > 0) m = __builtin_elementwise_max(m, *reinterpret_cast<const half8*>(vr + crow_swz(2 * qc - 1, c8)));
-        *reinterpret_cast<half8*>(out + (((size_t)n * 64 + p) * 64 + qc) * 64 + c8 * 8) = m;
+        store16<WT>(out, (unsigned)(((((size_t)n * 64 + p) * 64 + qc) * 64 + c8 * 8) * 2), m);
       }
     };
     if (mfma_first) {
@@ -561,10 +561,11 @@ static int run_stem(const float* x, int B, int Cin, const _Float16* w, const flo
   return PA_OK;
 }
 
-template <int PBT, int D>
+template <int PBT, int D, bool WT = false>
 static int run_stem3(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,
                      hipStream_t s) {
-  hipLaunchKernelGGL((stem_pool3_fp16<PBT, D>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out);
+  PA_CHECK(!WT || (size_t)B * 64 * 64 * 64 * 2 < 0x7fffffffu, "stem: output over 2 GB");
+  hipLaunchKernelGGL((stem_pool3_fp16<PBT, D, WT>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -594,7 +595,8 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     case 10: return run_stem3<8, 3>(x, B, Cin, w, bias, out, s);
     case 11: return run_stem3<16, 3>(x, B, Cin, w, bias, out, s);
     case 12: return run_stem3<32, 3>(x, B, Cin, w, bias, out, s);
-    default: return run_stem3<16, 2>(x, B, Cin, w, bias, out, s);
+    case 13: return run_stem3<16, 2, false>(x, B, Cin, w, bias, out, s);  // plain (write-back) stores
+    default: return run_stem3<16, 2, true>(x, B, Cin, w, bias, out, s);
   }
 }
 

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--layer", type=int, required=True)
+    p.add_argument("--layer", type=int, nargs="+", required=True)
     p.add_argument("--variant", type=int, required=True)
     p.add_argument("--launch", type=int, nargs="+", required=True)
     p.add_argument("--batch", type=int, default=64)
@@ -32,14 +32,16 @@ def main():
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
     x = torch.from_numpy(synth.synthetic_frames(0, a.batch)).cuda()
     buf = torch.zeros(24 * 65536, dtype=torch.int64, device="cuda")
-    _lib.check(L.pa_debug_set_variant(a.layer, a.variant))
+    for layer in a.layer:
+        _lib.check(L.pa_debug_set_variant(layer, a.variant))
     _lib.check(L.pa_debug_set_trace(buf.data_ptr()))
     for _ in range(a.runs):
         buf.zero_()
         m(x)
         torch.cuda.synchronize()
     _lib.check(L.pa_debug_set_trace(None))
-    L.pa_debug_set_variant(a.layer, 0)
+    for layer in a.layer:
+        L.pa_debug_set_variant(layer, 0)
     t = buf.view(24, -1, 64).cpu().numpy()
     for li in a.launch:
         tl = t[li]
