@@ -29,7 +29,7 @@ __device__ __forceinline__ void store16(void* base, unsigned off, half8 v) {
 
 // one s_memrealtime stamp per workgroup (thread 0) into slot `slot`
 __device__ __forceinline__ void trace_stamp(unsigned long long* tr, int slot) {
-  if (threadIdx.x == 0 && slot < TRACE_SLOTS) tr[blockIdx.x * TRACE_SLOTS + slot] = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && slot < TRACE_SLOTS) tr[(blockIdx.y * gridDim.x + blockIdx.x) * TRACE_SLOTS + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 struct ConvArgs {
@@ -58,8 +58,6 @@ struct ConvS2Args {
 template <typename T>
 int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname);
 
-// persistent fp16 variant (conv_s2p.hip), layer2/3
-int launch_conv3x3s2_ds_p(const ConvS2Args& a, int variant, hipStream_t s);
 
 // fp16, LDS-DMA deep ring (conv_s2x.h, conv_s2x_l.hip), layers 2-4
 int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
@@ -70,8 +68,6 @@ int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);
 template <typename T>
 int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname);
 
-// 3x3 s1, fp16, LDS-DMA staging with counted vmcnt (conv_glds.hip)
-int launch_conv3x3_glds(const ConvArgs& a, int variant, hipStream_t s);
 
 // 3x3 s1, fp16, LDS-DMA with a deep weight ring, fully unrolled (conv_gx.h, conv_gx_l*.hip)
 int launch_conv3x3_gx_l2(const ConvArgs& a, int variant, hipStream_t s);
@@ -83,8 +79,6 @@ int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s);
 // the same with LDS-DMA staging spread through the K loop (conv_c64d.hip)
 int launch_conv3x3_c64d(const ConvArgs& a, int variant, hipStream_t s);
 
-template <typename T>
-int launch_conv3x3_pipe(const ConvArgs& a, int variant, hipStream_t s);
 
 template <typename T>
 int launch_stem(const float* x, int B, int Cin, const T* w, const float* bias, T* out, hipStream_t s);

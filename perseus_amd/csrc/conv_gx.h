@@ -1,6 +1,10 @@
 // 3x3 stride-1 conv, fp16, LDS-DMA staging with a deep weight ring (the layer2-4
-// BasicBlock convs).  Same LDS images, MFMA roles and register epilogue as
-// conv_glds.hip, with three changes:
+// BasicBlock convs).  LDS images: 128-byte rows (one pixel's or one output
+// channel's 64 fp16 of the current 64-channel block), 16-byte chunks XOR-swizzled
+// by (row >> 1) & 7; the halo patch is DMA'd with the swizzle applied to the
+// per-lane source address.  MFMA A = weights, B = pixels; register epilogue.  An
+// earlier version of this kernel (distance-2 ring, looped K) measured 22 us on
+// layer3 against this one's 19.5.  The design points:
 //
 //  * prefetch distance PD: the weight tile of step s + PD is DMA'd at step s into
 //    a ring of PD + G slots (G = steps per barrier, below).  An L2-hit LDS-DMA under load takes about a

@@ -409,18 +409,10 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
   PA_CHECK(a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout, "patch conv: stride-1 only");
   PA_CHECK(a.Cin % PElem<T>::KB == 0, "patch conv: Cin %d", a.Cin);
   if (a.B <= 0) return PA_OK;
-  {
-    const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : 4;
-    if (g_variant[layer] >= 10 && g_variant[layer] < 30) {
-      static const char* names[5] = {"", "conv3x3q_l1", "conv3x3q_l2", "conv3x3q_l3", "conv3x3q_l4"};
-      if (kname) *kname = names[layer];
-      return launch_conv3x3_pipe<T>(a, g_variant[layer] - 10, s);
-    }
-  }
   if constexpr (std::is_same<T, _Float16>::value) {
     const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : 4;
     // layers 2-4: conv_gx (deep-ring LDS-DMA, inline-asm DMA, fully unrolled);
-    // variants 50-57 pick its alternatives, 40-43 the older conv_glds kernel
+    // variants 50-59 pick its alternatives
     if (layer >= 2 && (g_variant[layer] == 0 || (g_variant[layer] >= 50 && g_variant[layer] <= 59))) {
       static const char* names[5] = {"", "conv3x3x_l1", "conv3x3x_l2", "conv3x3x_l3", "conv3x3x_l4"};
       if (kname) *kname = names[layer];
@@ -428,12 +420,6 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       if (a.Cin == 128 && a.Hout == 32) return launch_conv3x3_gx_l2(a, v, s);
       if (a.Cin == 256 && a.Hout == 16) return launch_conv3x3_gx_l3(a, v, s);
       if (a.Cin == 512 && a.Hout == 8) return launch_conv3x3_gx_l4(a, v, s);
-    }
-    const int gv = g_variant[layer] >= 40 && g_variant[layer] <= 43 ? g_variant[layer] - 40 : -1;
-    if (gv >= 0) {
-      static const char* names[5] = {"", "conv3x3g_l1", "conv3x3g_l2", "conv3x3g_l3", "conv3x3g_l4"};
-      if (kname) *kname = names[layer];
-      return launch_conv3x3_glds(a, gv, s);
     }
     // layer1: the weight-resident persistent kernel for all four convs (variant 32
     // keeps the patch kernel for reference timing)

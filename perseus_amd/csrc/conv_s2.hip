@@ -312,14 +312,10 @@ template <typename T>
 int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
   if constexpr (std::is_same<T, _Float16>::value) {
-    // conv_s2x (shipped; g_variant[6] = 10..17 its alternatives); 1, 2: the
-    // persistent conv_s2p kernel (layer2/3); 3: the one-tile kernel below
+    // conv_s2x (shipped; g_variant[6] = 10..19 its alternatives); 3: the one-tile
+    // kernel below (bit-identical reference for the variant test)
     if (g_variant[6] == 0 || (g_variant[6] >= 10 && g_variant[6] <= 19))
       return launch_conv3x3s2_x(a, g_variant[6] == 0 ? 0 : g_variant[6] - 10, s, kname);
-    if (g_variant[6] != 3 && (a.Hout == 32 || a.Hout == 16)) {
-      if (kname) *kname = a.Hout == 32 ? "conv3x3s2p_l2" : "conv3x3s2p_l3";
-      return launch_conv3x3s2_ds_p(a, g_variant[6] == 2 ? 1 : 0, s);
-    }
   }
   if (a.Hout == 32) {
     if (kname) *kname = "conv3x3s2ds_l2";

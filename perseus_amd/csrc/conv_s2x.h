@@ -1,7 +1,7 @@
 // Stride-2 BasicBlock entry on conv_gx.h's machinery, fp16: conv 3x3 s2 (+ bn1,
 // relu) and the 1x1 s2 downsample (+ bn) in one pass over the input
-// (torchvision resnet18 layer2/3/4 block 0; replaces
-// conv_s2.hip / conv_s2p.hip on the fp16 path).
+// (torchvision resnet18 layer2/3/4 block 0; replaces the
+// one-tile kernel of conv_s2.hip on the fp16 path).
 //
 // The downsample reads input pixel (2y, 2x), the centre tap of the 3x3 window of
 // output (y, x): per 64-channel input block the K loop has 10 steps, the 9 taps
