@@ -31,8 +31,8 @@ REPS = 20  # back-to-back launches per timed launch in the per-kernel pass
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
     p.add_argument("--seed", type=int, default=0)
@@ -81,7 +81,7 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(args.steps):
-            kp[i] = model(x)
+            model(x, out=kp[i])  # keypoints straight into the step's slot
         if world > 1:  # one RCCL all-gather of every rank's keypoints (configs[2])
             shard.gather_keypoints(kp.view(-1, kp.shape[-1]))
         torch.cuda.synchronize(dev)
@@ -147,7 +147,7 @@ def main():
     return line
 
 
-def conv_flops(B, fused_stem=True, fused_ds=True):
+def conv_flops(B, fused_stem=True, fused_ds=True, fused_head=True):
     """Algorithmic FLOPs per launch, in forward order (matches pa_detector_profile)."""
     stem = 2.0 * B * 128 * 128 * 64 * 49 * 4  # true K = 196
     fl = [stem] if fused_stem else [stem, 0.0]  # fp16 fuses conv7x7 + maxpool
@@ -166,15 +166,19 @@ def conv_flops(B, fused_stem=True, fused_ds=True):
             fl.append(2.0 * B * ho * ho * cout * 9 * cout)          # conv2
             hw = ho
         cin = cout
-    fl.append(2.0 * B * 512 * 16)
+    if fused_head:  # avgpool + fc in layer4's last conv epilogue
+        fl[-1] += 2.0 * B * 512 * 16
+    else:
+        fl.append(2.0 * B * 512 * 16)
     return fl
 
 
 def roofline(per_launch, B, precision):
     fl = None
+    fused_head = per_launch[-1][1] != "avgpool_fc"
     for fs in (True, False):
         for fd in (True, False):
-            c = conv_flops(B, fused_stem=fs, fused_ds=fd)
+            c = conv_flops(B, fused_stem=fs, fused_ds=fd, fused_head=fused_head)
             if len(c) == len(per_launch):
                 fl = c
                 break

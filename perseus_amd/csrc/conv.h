@@ -5,7 +5,9 @@
 
 namespace pa {
 
-enum { EPI_RELU = 1, EPI_RES = 2 };
+// EPI_HEAD (layer4's last conv, conv_gx.h): avgpool + fc in the epilogue instead of the
+// activation store (models.py:31-32)
+enum { EPI_RELU = 1, EPI_RES = 2, EPI_HEAD = 4 };
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 extern int g_variant[8];  // kernel-variant selector per layer (A/B timing; 0 = shipped)
@@ -40,6 +42,13 @@ struct ConvArgs {
   void* out;          // NHWC [B][Hout][Wout][Cout]
   int B, Hin, Win, Cin, Hout, Wout, Cout, stride, pad, epi, M;
   unsigned long long* trace;  // timing-only variants: s_memrealtime stamps, TRACE_SLOTS per workgroup
+  // EPI_HEAD only: pooled means [B][Cout] f32, per-image-pair arrival counters (zero
+  // between launches), fc weight [16][Cout] / bias [16], keypoints out [B][16]
+  float* pool;
+  unsigned* cnt;
+  const float* fcw;
+  const float* fcb;
+  float* y;
 };
 
 // conv3x3 s2 (+bn, relu) -> out and 1x1 s2 downsample (+bn) -> out2, one pass

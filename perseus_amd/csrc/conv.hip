@@ -567,7 +567,7 @@ int launch_head(const T* in, int B, int HW, int C, const float* fcw, const float
   PA_CHECK(C == 512 && nout <= 32, "head: C=%d nout=%d", C, nout);  // 4 pixel groups x 64 chunks
   if (B <= 0) return PA_OK;
   if constexpr (std::is_same<T, _Float16>::value) {
-    if (HW == 64 && nout == 16 && g_variant[7] == 0) {
+    if (HW == 64 && nout == 16 && g_variant[7] != 1) {  // 1: the generic head_kernel
       hipLaunchKernelGGL(head_fp16<16>, dim3(B), dim3(256), 0, s, in, fcw, fcb, y);
       PA_LAUNCH_CHECK();
       return PA_OK;

@@ -114,6 +114,105 @@ struct GxPlan {
   }
 };
 
+// Fused avgpool + fc (models.py:31-32) for layer4's last conv, EPI_HEAD.  The workgroup
+// holds two whole 8x8 images x BN channels.  Its rounded fp16 outputs go to LDS instead
+// of HBM; the per-channel means are formed with head_fp16's exact arithmetic (conv.hip:
+// column sums over pixels g, g+4, .., g+60 in order, then (s0 + s1 + s2 + s3) / 64) and
+// written to a.pool; the last of the Cout / BN workgroups of the image pair to arrive
+// (agent-scope counter, reset by that workgroup) runs the fc exactly as head_fp16 does,
+// so the keypoints are bit-identical to the separate head.  No workgroup waits on another.
+template <int TH, int TW, int NI, int BN, int NT, int WTM, int WTN, int TM, int TN, int EPI>
+__device__ __forceinline__ void gx_head(const ConvArgs& a, char* smem, const f32x4 (&acc)[TM][TN],
+                                        const f32x4 (&bias)[TN], const half8 (&rv)[TM][TN / 2], int img0, int n0,
+                                        int ntn, int o) {
+  static_assert(TH == 8 && TW == 8 && NI == 2 && BN == 64 && NT == 512, "fused head: 2 whole 8x8 images x 64 ch");
+  constexpr int NOUT = 16, HW = 64;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q = lane >> 4;
+  constexpr int WN = BN / WTN;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  _Float16* tile = reinterpret_cast<_Float16*>(smem);  // [img][pixel][BN]
+  float* part = reinterpret_cast<float*>(smem + NI * HW * BN * 2);  // [img][wave][NOUT]
+  int* flag = reinterpret_cast<int*>(part + NI * 4 * NOUT);
+  __syncthreads();  // every wave is past its last fragment read
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int mb = wm * WTM + tm * 16;
+    const int pix = (o >> 3) * HW + (mb / 16) * TW + (o & 7);
+#pragma unroll
+    for (int p = 0; p < TN / 2; ++p) {
+      half8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = acc[tm][2 * p + (j >> 2)][j & 3] + bias[2 * p + (j >> 2)][j & 3];
+        if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
+        hv[j] = (_Float16)fmaxf(v, 0.f);
+      }
+      *reinterpret_cast<half8*>(tile + pix * BN + wn * WTN + p * 32 + q * 8) = hv;
+    }
+  }
+  // the fc weights of this thread's channel pair (t = tid & 255: channels 2t, 2t + 1),
+  // in flight during the pooling; only the pair's last workgroup uses them
+  const int t = tid & 255, wi = (tid >> 6) & 3, im = tid >> 8;
+  const int Cout = a.Cout;
+  float2 fw[NOUT];
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) fw[j] = *reinterpret_cast<const float2*>(a.fcw + (size_t)j * Cout + 2 * t);
+  // LDS-only barrier: __syncthreads() would also wait for the fc weight loads
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // thread (image, channel) < NI * BN: head_fp16's 4 pixel-group sums (pixels g, g + 4, ..,
+  // g + 60 in order) as 4 independent chains; lanes read consecutive channels (no conflicts)
+  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(a.pool, 0, 0x7fffffff, 0x00020000);
+  if (tid < NI * BN) {
+    const int pim = tid / BN, c = tid % BN;
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < HW / 4; ++u)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) cs[g] += (float)tile[(pim * HW + g + 4 * u) * BN + c];
+    const float inv = 1.0f / (float)HW;
+    const float mean = (cs[0] + cs[1] + cs[2] + cs[3]) * inv;
+    const int pn = img0 + pim;
+    if (pn < a.B)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mean), pr,
+                                            (int)(((size_t)pn * Cout + n0 + c) * 4), 0, 16);
+  }
+  const int n = img0 + im;
+  // hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the means are stored
+  // write-through (sc1), every wave drains its stores, one lane adds to the pair's
+  // agent-scope counter; the last arriver reads them with sc1 loads.  No __threadfence
+  // (an L2 write-back per workgroup: 21 -> 63 us for this launch when tried).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    unsigned* ctr = a.cnt + img0 / NI;
+    const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(ntn - 1);
+    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch (stream order)
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  // fc, head_fp16's arithmetic: thread t of image im takes channels 2t, 2t + 1
+  if (n < a.B) {  // wave-uniform (im = tid >> 8)
+    const float2 m = __builtin_bit_cast(
+        float2, __builtin_amdgcn_raw_buffer_load_b64(pr, (int)(((size_t)n * Cout + 2 * t) * 4), 0, 16));
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) {
+      float v = fmaf(fw[j].y, m.y, fw[j].x * m.x);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) part[(im * 4 + wi) * NOUT + j] = v;
+    }
+  }
+  __syncthreads();
+  if (t < NOUT && n < a.B) {
+    const float* pp = part + im * 4 * NOUT;
+    a.y[(size_t)n * NOUT + t] = pp[t] + pp[NOUT + t] + pp[2 * NOUT + t] + pp[3 * NOUT + t] + a.fcb[t];
+  }
+}
+
 // DBG (timing experiments only, wrong results): 1 = no waits / barriers in the K loop,
 // 2 = also no weight / patch DMAs in the K loop, 3 = no K loop (prologue + epilogue);
 // 4 = the shipped kernel plus s_memrealtime stamps into a.trace (conv.h trace_stamp)
@@ -338,6 +437,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   if constexpr (DBG == 4) trace_stamp(a.trace, 2);
   xwait_vm<0>();  // bias / residual (also waited for by the compiler at their use)
 
+  if constexpr (EPI & EPI_HEAD) {
+    gx_head<TH, TW, NI, BN, NT, WTM, WTN, TM, TN, EPI>(a, smem, acc, bias, rv, img0, n0, ntn, o);
+    return;
+  }
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     if (!ok[tm]) continue;
@@ -363,7 +466,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1,
           bool WT = true>
 static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
-  PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "gx conv: epilogue %d", a.epi);
+  PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES) || a.epi == (EPI_RELU | EPI_RES | EPI_HEAD),
+           "gx conv: epilogue %d", a.epi);
   PA_CHECK(a.Cin == CIN, "gx conv: Cin %d != %d", a.Cin, CIN);
   PA_CHECK(a.Hout % TH == 0 && a.Wout % TW == 0, "gx conv: %dx%d not tiled by %dx%d", a.Hout, a.Wout, TH, TW);
   PA_CHECK(a.Cout % BN == 0, "gx conv: Cout %d %% BN %d", a.Cout, BN);
@@ -372,7 +476,15 @@ static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
   const int tiles = nsp * ntn;
   const int x = xg && nsp % 8 == 0;  // whole groups of 8 spatial tiles only
   PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 < 0x7fffffffu, "gx conv: output over 2 GB");
-  if (a.epi & EPI_RES)
+  if (a.epi & EPI_HEAD) {
+    if constexpr (TH == 8 && TW == 8 && NI == 2 && BN == 64 && WM * WN == 8 && DBG == 0) {
+      PA_CHECK(a.pool && a.cnt && a.fcw && a.fcb && a.y && a.Cout == 512, "gx conv: fused head arguments");
+      hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES | EPI_HEAD, DBG, FD, WT>),
+                         dim3(tiles), dim3(WM * WN * 64), 0, s, a, x);
+    } else {
+      PA_CHECK(false, "gx conv: fused head needs the 2 x 8x8 x 64-channel tile");
+    }
+  } else if (a.epi & EPI_RES)
     hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT>), dim3(tiles),
                        dim3(WM * WN * 64), 0, s, a, x);
   else

@@ -415,7 +415,7 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
     // variants 50-59 pick its alternatives
     if (layer >= 2 && (g_variant[layer] == 0 || (g_variant[layer] >= 50 && g_variant[layer] <= 59))) {
       static const char* names[5] = {"", "conv3x3x_l1", "conv3x3x_l2", "conv3x3x_l3", "conv3x3x_l4"};
-      if (kname) *kname = names[layer];
+      if (kname) *kname = (a.epi & EPI_HEAD) ? "conv3x3x_l4_avgpool_fc" : names[layer];
       const int v = g_variant[layer] == 0 ? 0 : g_variant[layer] - 50;
       if (a.Cin == 128 && a.Hout == 32) return launch_conv3x3_gx_l2(a, v, s);
       if (a.Cin == 256 && a.Hout == 16) return launch_conv3x3_gx_l3(a, v, s);

@@ -49,6 +49,9 @@ struct pa_detector {
   float* fcb = nullptr;
   char* ws = nullptr;
   size_t ws_bytes = 0;
+  float* pool = nullptr;     // fused head: pooled means [cap][512] f32
+  unsigned* cnt = nullptr;   // fused head: per-image-pair arrival counters, zero between launches
+  int head_cap = 0;          // batch capacity of pool / cnt
   double flops_per_frame = 0;
   int device = 0;
 };
@@ -162,7 +165,13 @@ static size_t ws_need(int B, int prec) {
   return (stem + 3 * act) * es + 1024;
 }
 
+static int ensure_head(pa_detector* d, int B);
+
 static int ensure_ws(pa_detector* d, int B) {
+  {
+    const int rc = ensure_head(d, B);
+    if (rc != PA_OK) return rc;
+  }
   const size_t need = ws_need(B, d->prec);
   if (need <= d->ws_bytes) return PA_OK;
   if (d->ws) {
@@ -176,6 +185,27 @@ static int ensure_ws(pa_detector* d, int B) {
     return PA_ENOMEM;
   }
   d->ws_bytes = need;
+  return PA_OK;
+}
+
+// fused avgpool + fc (conv_gx.h gx_head): pooled means and zeroed arrival counters
+static int ensure_head(pa_detector* d, int B) {
+  if (B <= d->head_cap) return PA_OK;
+  if (d->pool) PA_HIP(hipFree(d->pool));
+  if (d->cnt) PA_HIP(hipFree(d->cnt));
+  d->pool = nullptr;
+  d->cnt = nullptr;
+  d->head_cap = 0;
+  const int npair = (B + 1) / 2;
+  if (hipMalloc(&d->pool, (size_t)B * 512 * sizeof(float)) != hipSuccess ||
+      hipMalloc(&d->cnt, (size_t)npair * sizeof(unsigned)) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("head workspace: hipMalloc failed");
+    return PA_ENOMEM;
+  }
+  PA_HIP(hipMemset(d->cnt, 0, (size_t)npair * sizeof(unsigned)));
+  PA_HIP(hipDeviceSynchronize());
+  d->head_cap = B;
   return PA_OK;
 }
 
@@ -241,6 +271,13 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   T* X = S + stem_el;
   T* Tb = X + act_el;
   T* D = Tb + act_el;
+  // g_variant[7] == 3: avgpool + fc fused into layer4's last conv (conv_gx.h gx_head).
+  // Bit-identical to the separate head_fp16 and measured neutral (27.3 us for the fused
+  // launch vs 19.5 + 6.7 us; 176.7k vs 177.3k frames/s interleaved), so not shipped.
+  bool fuse_head = false;
+  if constexpr (std::is_same<T, _Float16>::value)
+    fuse_head = g_variant[7] == 3 && g_variant[4] == 0 && d->n_kp == 8 && d->H == 256 && d->W == 256 &&
+                d->blocks.back().ds < 0;
   if (prof) prof->mark("start");
   const ConvL& st = d->convs[0];
   if constexpr (std::is_same<T, _Float16>::value) {
@@ -338,11 +375,19 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     b2.pad = 1;
     b2.epi = EPI_RELU | EPI_RES;
     b2.trace = trace();
+    if (fuse_head && &b == &d->blocks.back()) {
+      b2.epi |= EPI_HEAD;
+      b2.pool = d->pool;
+      b2.cnt = d->cnt;
+      b2.fcw = d->fcw;
+      b2.fcb = d->fcb;
+      b2.y = y;
+    }
     PA_RUN(launch_conv3x3_s1<T>(b2, s, &kn), kn);
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
   }
-  PA_RUN(launch_head<T>(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s), "avgpool_fc");
+  if (!fuse_head) PA_RUN(launch_head<T>(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s), "avgpool_fc");
   return PA_OK;
 }
 
@@ -401,6 +446,8 @@ void pa_detector_destroy(pa_detector* d) {
   hipFree(d->fcw);
   hipFree(d->fcb);
   if (d->ws) hipFree(d->ws);
+  if (d->pool) hipFree(d->pool);
+  if (d->cnt) hipFree(d->cnt);
   delete d;
 }
 

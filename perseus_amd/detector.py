@@ -181,14 +181,23 @@ class KeypointCNN(nn.Module):
         x = x.to(torch.float32).contiguous()
         return x, out_dev
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """`out` (optional, not in the reference signature): a contiguous f32 (B, 16) tensor on
+        the input's GPU that the keypoints are written into (no extra copy kernel)."""
         x, out_dev = self._prep(x)
         dev = x.device
         h = self._ensure_handle(dev)
         L = _lib.lib()
         _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP32 if self.precision == "fp32" else _lib.PREC_FP16),
                    "set_precision")
-        y = torch.empty((x.shape[0], 2 * self.n_keypoints), dtype=torch.float32, device=dev)
+        shape = (x.shape[0], 2 * self.n_keypoints)
+        if out is not None:
+            if (out.device != dev or out.dtype != torch.float32 or tuple(out.shape) != shape
+                    or not out.is_contiguous()):
+                raise RuntimeError(f"out must be a contiguous float32 {shape} tensor on {dev}")
+            y = out
+        else:
+            y = torch.empty(shape, dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
             _lib.check(L.pa_detector_forward(h, x.data_ptr(), x.shape[0], y.data_ptr(), _lib.stream_of(dev)),
                        "pa_detector_forward")

@@ -141,6 +141,15 @@ def test_profile_reports_every_kernel():
     assert len(names) == 1 + 4 + 4 + 4 + 4 + 1  # stride-2 conv1 + 1x1 downsample fused
     assert names[5].startswith("conv3x3s2")
     assert torch.equal(y, m(x))
+    from perseus_amd import _lib
+
+    L = _lib.lib()
+    try:
+        _lib.check(L.pa_debug_set_variant(7, 3))  # avgpool + fc fused into layer4's last conv
+        names_fused = [n for n, _ in m.profile(x)[0]]
+    finally:
+        L.pa_debug_set_variant(7, 0)
+    assert names_fused[-1] == "conv3x3x_l4_avgpool_fc" and len(names_fused) == len(names) - 1
     m.precision = "fp32"
     prof32, _ = m.profile(x)
     assert [n for n, _ in prof32][:2] == ["stem_conv7x7", "maxpool"]
@@ -162,6 +171,7 @@ def test_kernel_variants_agree_bit_for_bit(B):
         ((1, 3), (2, 1), (3, 1), (4, 1), (6, 3), (0, 10)),
         ((1, 30), (7, 1)),  # layer1: register-staged kernel on every conv; the generic head
         ((1, 60),),  # layer1: LDS-DMA kernel on every conv
+        ((7, 3),),  # avgpool + fc fused into layer4's last conv instead of head_fp16
     )
     for vs in sets:
         try:
@@ -172,3 +182,38 @@ def test_kernel_variants_agree_bit_for_bit(B):
             for layer in range(8):
                 L.pa_debug_set_variant(layer, 0)
         assert torch.equal(y0, y1), vs
+
+
+def test_forward_into_out_buffer():
+    """forward(x, out=buf) writes the same keypoints into buf (bench.py's step) and rejects a bad buffer."""
+    m = model(0)
+    x = torch.from_numpy(synth.synthetic_frames(0, 4)).cuda()
+    ref = m(x)
+    buf = torch.full((2, 4, 16), float("nan"), device="cuda")
+    got = m(x, out=buf[1])
+    assert got.data_ptr() == buf[1].data_ptr()
+    assert torch.equal(buf[1], ref) and torch.isnan(buf[0]).all()
+    with pytest.raises(RuntimeError):
+        m(x, out=torch.empty((4, 16), dtype=torch.float16, device="cuda"))
+    with pytest.raises(RuntimeError):
+        m(x, out=torch.empty((16, 4), device="cuda").t())
+
+
+def test_fused_head_repeats_and_batch_changes():
+    """The fused head (variant 7:3) keeps per-image-pair counters that return to zero after
+    every launch: repeated forwards, odd batches and a batch larger than the last reserve all
+    give the separate head's bits."""
+    from perseus_amd import _lib
+
+    L = _lib.lib()
+    m = model(1)
+    for B in (2, 5, 64, 7, 130):
+        x = torch.from_numpy(synth.synthetic_frames(3, B)).cuda()
+        ref = m(x)
+        try:
+            _lib.check(L.pa_debug_set_variant(7, 3))
+            ys = [m(x) for _ in range(3)]
+        finally:
+            L.pa_debug_set_variant(7, 0)
+        for y in ys:
+            assert torch.equal(y, ref), B

@@ -7,7 +7,7 @@ rc=$?
 echo pytest_rc=$rc
 grep -E "passed|failed|error" gpurun_out/pytest_gpu.log | tail -3
 if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 ${BENCH_TIMEOUT:-300} python bench.py ${BENCH_ARGS:---steps 30 --warmup 10} > gpurun_out/bench.log 2>&1
+timeout -k 10 ${BENCH_TIMEOUT:-300} python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?
 echo bench_rc=$rc
 tail -1 gpurun_out/bench.log

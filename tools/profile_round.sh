@@ -5,7 +5,7 @@
 # host with tools/rocprof_summary.py --dir gpurun_out/<tag> --tag <tag>.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-prof}
-BENCH_ARGS=${BENCH_ARGS:---steps 30 --warmup 10}
+BENCH_ARGS=${BENCH_ARGS:-}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
