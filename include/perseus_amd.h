@@ -108,6 +108,16 @@ int pa_preprocess_rgbd(const uint8_t* rgb_dev, const float* depth_dev, int B, in
 int pa_keypoints_postprocess(const float* y_dev, const float* target_dev, int B, int n_kp, int H, int W,
                              float* px_dev, float* loss_dev, void* stream);
 
+/* Validation loss statistics (validate.py:162-168, the "Validation Loss" block):
+ * over n f32 losses on the device, stats_dev[0..4] (f64, device) = mean, stdev
+ * (unbiased, torch.std; NaN for n = 1), min, max, median (torch.median: the
+ * element of sorted index (n-1)/2).  ws_dev: device scratch of
+ * pa_loss_statistics_workspace(n) bytes, 16-byte aligned.  Stream-ordered, no
+ * host sync.  n must be > 0 (torch.median raises on an empty tensor). */
+size_t pa_loss_statistics_workspace(long long n);
+int pa_loss_statistics(const float* loss_dev, long long n, double* stats_dev, void* ws_dev, size_t ws_bytes,
+                       void* stream);
+
 /* ------------------------------------------------------------------- factors */
 /* Pose encoding: 12 f64 per pose = R row-major (9) then t (3).  Jacobians are
  * column-major per factor (Eigen/GTSAM order), tangent order [omega; v].

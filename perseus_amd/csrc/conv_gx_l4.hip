@@ -10,6 +10,8 @@ int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s) {
   const bool xg = !(variant & 4);
   if (variant == 6) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 0, 1, false>(a, true, s);  // plain (write-back) stores
   if (variant == 7 && a.trace) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 4>(a, true, s);  // timestamps
+  if (variant == 8) return run_gx<8, 8, 2, 64, 2, 2, 512, 4>(a, xg, s);  // 4 waves of 64x32 (1 per SIMD)
+  if (variant == 9) return run_gx<8, 8, 2, 64, 2, 2, 512, 6>(a, xg, s);  // same, weight ring distance 6
   switch (variant & 3) {
       case 1: return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 2>(a, xg, s);
       case 2: return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 3>(a, xg, s);

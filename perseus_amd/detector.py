@@ -259,6 +259,26 @@ def denormalize_pixel_coordinates(y: torch.Tensor, H: int = 256, W: int = 256, t
     return px if loss is None else (px, loss)
 
 
+def loss_statistics(losses: torch.Tensor) -> dict:
+    """The "Validation Loss" block of validate.py:162-168 on the device: mean, stdev
+    (unbiased, as torch.std), min, max and median (torch.median: the lower middle element)
+    of the flattened losses, computed by the library's HIP kernels (pa_loss_statistics)
+    with one device->host copy of the five results.  Raises on an empty tensor."""
+    if losses.device.type != "cuda":
+        raise RuntimeError("loss_statistics expects a device tensor")
+    x = losses.reshape(-1).contiguous().float()
+    n = x.numel()
+    if n == 0:
+        raise RuntimeError("loss_statistics: empty input")
+    L = _lib.lib()
+    ws = torch.empty(int(L.pa_loss_statistics_workspace(n)), dtype=torch.uint8, device=x.device)
+    out = torch.empty(5, dtype=torch.float64, device=x.device)
+    _lib.check(L.pa_loss_statistics(x.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                    _lib.stream_of(x.device)), "loss_statistics")
+    mean, std, mn, mx, med = out.cpu().tolist()
+    return {"mean": mean, "std": std, "min": mn, "max": mx, "median": med}
+
+
 def preprocess_rgbd(rgb: torch.Tensor, depth: torch.Tensor, H: int = 256, W: int = 256, bgr: bool = True,
                     near: float | None = None, far: float | None = None) -> torch.Tensor:
     """Device version of ZEDCamera.get_frame's arithmetic (streaming.py:59-82) +
