@@ -68,6 +68,15 @@ int pa_detector_set_precision(pa_detector* d, int precision);
  * normalized image coordinates.  B = 0 is a no-op. */
 int pa_detector_forward(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream);
 
+/* Camera frames -> keypoints in one pass: uint8 HWC RGB (bgr != 0: BGR
+ * byte order, as the ZED delivers) + f32 depth in metres, both [B][Hs][Ws], centre-cropped
+ * to 256x256; pa_preprocess_rgbd's arithmetic (streaming.py:68-80, deterministic near/far
+ * clip, < 0 = off) is applied inside the stem's row loads, so the f32 (B,4,256,256) input
+ * is never written.  Output bit-identical to pa_preprocess_rgbd + pa_detector_forward.
+ * fp16 precision and 4-channel models only (PA_EINVAL otherwise). */
+int pa_detector_forward_rgbd(pa_detector* d, const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws,
+                             int bgr, float near_m, float far_m, float* y_dev, void* stream);
+
 /* Same forward with a HIP event after every kernel: writes up to max_n per-kernel
  * durations (ms) into ms_out and their names into names_out (may be NULL), returns
  * the number of kernels or <0.  Synchronises the stream (diagnostics only). */

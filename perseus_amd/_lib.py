@@ -56,6 +56,8 @@ _SIGS = {
                                      C.c_float, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "pa_keypoints_postprocess": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                            C.c_void_p, C.c_void_p, C.c_void_p]),
+    "pa_detector_forward_rgbd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.c_float, C.c_float, C.c_void_p, C.c_void_p]),
     "pa_loss_statistics_workspace": (C.c_size_t, [C.c_longlong]),
     "pa_loss_statistics": (C.c_int, [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "pa_proj_linearize": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,

@@ -92,6 +92,17 @@ int launch_conv3x3_c64d(const ConvArgs& a, int variant, hipStream_t s);
 template <typename T>
 int launch_stem(const float* x, int B, int Cin, const T* w, const float* bias, T* out, hipStream_t s);
 
+// raw camera frames for the fused-preprocess stem (streaming.py:68-80; conv.hip
+// preprocess_kernel's arithmetic): uint8 HWC RGB/BGR + f32 depth [B][Hs][Ws], centre
+// crop to 256x256, near/far clip disabled when < 0
+struct RgbdSrc {
+  const uint8_t* rgb;
+  const float* depth;
+  int Hs, Ws, bgr;
+  float near_m, far_m;
+};
+int launch_stem_pool_rgbd(const RgbdSrc& src, int B, const _Float16* w, const float* bias, _Float16* out,
+                          hipStream_t s);
 int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,
                           hipStream_t s);
 

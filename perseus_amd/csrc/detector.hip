@@ -263,7 +263,8 @@ struct Prof {
   } while (0)
 
 template <typename T>
-static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof) {
+static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof,
+                     const RgbdSrc* rgbd = nullptr) {
   const T* wts = std::is_same<T, float>::value ? (const T*)d->w32 : (const T*)d->w16;
   T* S = reinterpret_cast<T*>(d->ws);
   const size_t stem_el = (size_t)B * 128 * 128 * 64;
@@ -282,7 +283,10 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   const ConvL& st = d->convs[0];
   if constexpr (std::is_same<T, _Float16>::value) {
     // fused conv7x7 + BN + ReLU + maxpool: the 128x128 map stays on chip
-    PA_RUN(launch_stem_pool_fp16(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, X, s), "stem_conv7x7_pool");
+    if (rgbd)  // camera frames straight into the stem (preprocess fused into its row loads)
+      PA_RUN(launch_stem_pool_rgbd(*rgbd, B, wts + st.w_off, d->bias + st.b_off, X, s), "stem_rgbd_conv7x7_pool");
+    else
+      PA_RUN(launch_stem_pool_fp16(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, X, s), "stem_conv7x7_pool");
   } else {
     PA_RUN(launch_stem<T>(x, B, d->in_ch, wts + st.w_off, d->bias + st.b_off, S, s), "stem_conv7x7");
     PA_RUN(launch_maxpool<T>(S, B, 128, 128, 64, X, s), "maxpool");
@@ -400,9 +404,29 @@ static int forward(pa_detector* d, const float* x, int B, float* y, hipStream_t 
   return d->prec == PA_PREC_FP32 ? forward_t<float>(d, x, B, y, s, prof) : forward_t<_Float16>(d, x, B, y, s, prof);
 }
 
+// camera frames -> keypoints, preprocess fused into the stem (fp16, 4-channel models)
+static int forward_rgbd(pa_detector* d, const RgbdSrc& src, int B, float* y, hipStream_t s) {
+  PA_CHECK(d, "null detector");
+  PA_CHECK(B >= 0, "batch %d", B);
+  if (B == 0) return PA_OK;
+  PA_CHECK(src.rgb && src.depth && y, "null input/output pointer");
+  PA_CHECK(d->prec == PA_PREC_FP16, "forward_rgbd: fused preprocess is the fp16 path (fp32: pa_preprocess_rgbd + "
+                                    "pa_detector_forward)");
+  PA_CHECK(d->in_ch == 4, "forward_rgbd: needs a 4-channel (RGBD) model, have %d", d->in_ch);
+  PA_CHECK(src.Hs >= 256 && src.Ws >= 256, "forward_rgbd: source %dx%d smaller than 256x256", src.Hs, src.Ws);
+  PA_TRY(ensure_ws(d, B));
+  return forward_t<_Float16>(d, nullptr, B, y, s, nullptr, &src);
+}
+
 }  // namespace pa
 
 extern "C" {
+
+int pa_detector_forward_rgbd(pa_detector* d, const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws,
+                             int bgr, float near_m, float far_m, float* y_dev, void* stream) {
+  const pa::RgbdSrc src{rgb_dev, depth_dev, Hs, Ws, bgr, near_m, far_m};
+  return pa::forward_rgbd(d, src, B, y_dev, (hipStream_t)stream);
+}
 
 const char* pa_last_error(void) { return pa::g_err.c_str(); }
 const char* pa_version(void) { return "perseus_amd 0.1 gfx950"; }

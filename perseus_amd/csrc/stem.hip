@@ -53,10 +53,14 @@ __device__ __forceinline__ void stem_for(F&& f) {
 // (all 7 kh x 64 channels, 112 VGPRs per lane) is loaded once, so the MFMA phase
 // reads only the input fragments from LDS.  One LDS-only barrier per pair; waves
 // 0-3 do MFMAs then pooling, waves 4-7 the other order (SIMD partners overlap).
-template <int PBT, int D, bool WT = false, int DBG = 0>
+// PRE: the input rows come straight from the camera frames (RgbdSrc) through
+// preprocess_kernel's arithmetic (conv.hip), so the f32 NCHW frame never exists; the
+// values reaching the fp16 ring are the same f32 numbers, hence bit-identical output.
+template <int PBT, int D, bool WT = false, int DBG = 0, bool PRE = false>
 __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__ x, int B, int Cin,
                                                        const _Float16* __restrict__ w, const float* __restrict__ bias,
-                                                       _Float16* __restrict__ out, unsigned long long* trace) {
+                                                       _Float16* __restrict__ out, unsigned long long* trace,
+                                                       RgbdSrc src) {
   using namespace stem;
   static_assert(RING >= 9 + 4 && D >= 2 && D <= 3, "ring / prefetch depth");
   constexpr int WSTAGE = RING * ROWB + 2 * CROWB + 64 * 4;  // 28 KB weight staging (A fragment order)
@@ -76,10 +80,40 @@ __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__
   const int lr = tid >> 7, lcg = (tid >> 1) & 63, lcp = tid & 1;
   auto load_rows = [&](int hi0, float4* v) __attribute__((always_inline)) {
     const int hi = min(max(hi0 + lr, 0), 255);
+    if constexpr (PRE) {
+      // 4 pixels of row hi, channels 2 lcp and 2 lcp + 1 (R,G or B,depth)
+      const int r0 = src.Hs / 2 - 128, c0 = src.Ws / 2 - 128;
+      const size_t row = ((size_t)n * src.Hs + hi + r0) * src.Ws + c0 + lcg * 4;
+      const int sc0 = lcp ? (src.bgr ? 0 : 2) : (src.bgr ? 2 : 0);  // channel 2 lcp
+      constexpr int sc1 = 1;                                        // channel 1 (lcp = 0)
+      float a0[4], a1[4];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int ch = min(2 * lcp + c, Cin - 1);
-      v[c] = *reinterpret_cast<const float4*>(xn + ((size_t)ch * 256 + hi) * 256 + lcg * 4);
+      for (int k = 0; k < 4; ++k) {
+        const uint8_t* px = src.rgb + (row + k) * 3;
+        a0[k] = (float)((double)px[sc0] / 255.0);  // numpy f64 /255 then .float()
+        if (lcp == 0) {
+          a1[k] = (float)((double)px[sc1] / 255.0);
+        } else {
+          float d = src.depth[row + k];
+          if (isnan(d) || isinf(d)) d = 0.f;
+          d = d / 0.035f;  // streaming.py:76
+          if (src.near_m >= 0.f || src.far_m >= 0.f) {
+            float sd = 0.035f * d;  // DepthPlaneAugmentation: scale, clip, unscale
+            if (src.near_m >= 0.f && sd < src.near_m) sd = 0.f;
+            if (src.far_m >= 0.f && sd > src.far_m) sd = 0.f;
+            d = sd / 0.035f;
+          }
+          a1[k] = d;
+        }
+      }
+      v[0] = float4{a0[0], a0[1], a0[2], a0[3]};
+      v[1] = float4{a1[0], a1[1], a1[2], a1[3]};
+    } else {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int ch = min(2 * lcp + c, Cin - 1);
+        v[c] = *reinterpret_cast<const float4*>(xn + ((size_t)ch * 256 + hi) * 256 + lcg * 4);
+      }
     }
   };
   auto store_rows = [&](int hi0, const float4* v) __attribute__((always_inline)) {
@@ -237,14 +271,22 @@ __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__
   }
 }
 
-template <int PBT, int D, bool WT = false, int DBG = 0>
+template <int PBT, int D, bool WT = false, int DBG = 0, bool PRE = false>
 static int run_stem3(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,
-                     hipStream_t s, unsigned long long* trace = nullptr) {
+                     hipStream_t s, unsigned long long* trace = nullptr, RgbdSrc src = RgbdSrc{}) {
   PA_CHECK(!WT || (size_t)B * 64 * 64 * 64 * 2 < 0x7fffffffu, "stem: output over 2 GB");
-  hipLaunchKernelGGL((stem_pool3_fp16<PBT, D, WT, DBG>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out,
-                     trace);
+  hipLaunchKernelGGL((stem_pool3_fp16<PBT, D, WT, DBG, PRE>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias,
+                     out, trace, src);
   PA_LAUNCH_CHECK();
   return PA_OK;
+}
+
+int launch_stem_pool_rgbd(const RgbdSrc& src, int B, const _Float16* w, const float* bias, _Float16* out,
+                          hipStream_t s) {
+  PA_CHECK(src.rgb && src.depth, "stem rgbd: null frame pointer");
+  PA_CHECK(src.Hs >= 256 && src.Ws >= 256, "stem rgbd: source %dx%d smaller than 256x256", src.Hs, src.Ws);
+  if (B <= 0) return PA_OK;
+  return run_stem3<16, 2, true, 0, true>(nullptr, B, 4, w, bias, out, s, nullptr, src);
 }
 
 int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,

@@ -203,6 +203,35 @@ class KeypointCNN(nn.Module):
                        "pa_detector_forward")
         return y if out_dev == dev else y.to(out_dev)
 
+    def forward_rgbd(self, rgb: torch.Tensor, depth: torch.Tensor, bgr: bool = True, near: float | None = None,
+                     far: float | None = None) -> torch.Tensor:
+        """Camera frames -> keypoints (streaming.py:68-80 then :128): uint8 (B,Hs,Ws,3) + f32
+        metres (B,Hs,Ws) on the GPU, centre-cropped to 256x256.  fp16: the preprocess runs
+        inside the stem's row loads (pa_detector_forward_rgbd, no f32 input tensor); fp32: the
+        separate pa_preprocess_rgbd kernel, then forward().  Both give the bits of
+        forward(preprocess_rgbd(rgb, depth, ...))."""
+        if rgb.device.type != "cuda" or depth.device.type != "cuda":
+            raise RuntimeError("forward_rgbd expects device tensors")
+        if self.precision == "fp32" or self.num_channels != 4:
+            return self.forward(preprocess_rgbd(rgb, depth, self.H, self.W, bgr=bgr, near=near, far=far))
+        rgb = rgb.contiguous()
+        depth = depth.contiguous().float()
+        if rgb.dtype != torch.uint8 or rgb.dim() != 4 or rgb.shape[-1] != 3 or depth.shape != rgb.shape[:3]:
+            raise RuntimeError(f"expected uint8 (B,Hs,Ws,3) + (B,Hs,Ws) depth, got {tuple(rgb.shape)} "
+                               f"{rgb.dtype} / {tuple(depth.shape)}")
+        B, Hs, Ws, _ = rgb.shape
+        dev = rgb.device
+        h = self._ensure_handle(dev)
+        L = _lib.lib()
+        _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP16), "set_precision")
+        y = torch.empty((B, 2 * self.n_keypoints), dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            _lib.check(L.pa_detector_forward_rgbd(h, rgb.data_ptr(), depth.data_ptr(), B, Hs, Ws, int(bgr),
+                                                  -1.0 if near is None else float(near),
+                                                  -1.0 if far is None else float(far), y.data_ptr(),
+                                                  _lib.stream_of(dev)), "pa_detector_forward_rgbd")
+        return y
+
     def profile(self, x: torch.Tensor, max_kernels: int = 64):
         """Per-kernel device times (ms) of one forward, via HIP events in the library."""
         x, _ = self._prep(x)

@@ -5,8 +5,9 @@ Mirrors the per-frame loop of `scripts/streaming.py:120-131` (grab BGR + depth,
 denormalize) for `n_cams` cameras per tick, batched into one forward.  Per tick:
 
   host: frames -> pinned staging (centre crop rows only, or the full frame)
-  GPU (one hipGraph replay on a private stream): H2D -> pa_preprocess_rgbd ->
-       pa_detector_forward (B = n_cams) -> pa_keypoints_postprocess -> D2H pixels
+  GPU (one hipGraph replay on a private stream): H2D -> pa_detector_forward_rgbd
+       (B = n_cams; the preprocess runs inside the stem's row loads; fp32: pa_preprocess_rgbd
+       + pa_detector_forward) -> pa_keypoints_postprocess -> D2H pixels
   host: wait for the replay, return (n_cams, K, 2) pixel coordinates.
 
 The graph removes the per-launch CPU cost of the ~22 launches (the forward at B=3
@@ -74,10 +75,15 @@ class StreamingPipeline:
         s = torch.cuda.current_stream(self.dev).cuda_stream
         self.rgb_d.copy_(self.rgb_h, non_blocking=True)
         self.depth_d.copy_(self.depth_h, non_blocking=True)
-        _lib.check(L.pa_preprocess_rgbd(self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n, self.sh, self.sw,
-                                        int(self.bgr), self.near, self.far, self.H, self.W, self.x.data_ptr(), s),
-                   "preprocess")
-        _lib.check(L.pa_detector_forward(self._h, self.x.data_ptr(), self.n, self.y.data_ptr(), s), "forward")
+        if self.model.precision == "fp32":
+            _lib.check(L.pa_preprocess_rgbd(self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n, self.sh, self.sw,
+                                            int(self.bgr), self.near, self.far, self.H, self.W, self.x.data_ptr(), s),
+                       "preprocess")
+            _lib.check(L.pa_detector_forward(self._h, self.x.data_ptr(), self.n, self.y.data_ptr(), s), "forward")
+        else:  # fp16: the preprocess runs inside the stem's row loads
+            _lib.check(L.pa_detector_forward_rgbd(self._h, self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n,
+                                                  self.sh, self.sw, int(self.bgr), self.near, self.far,
+                                                  self.y.data_ptr(), s), "forward_rgbd")
         _lib.check(L.pa_keypoints_postprocess(self.y.data_ptr(), None, self.n, self.model.n_keypoints, self.H, self.W,
                                               self.px_d.data_ptr(), None, s), "postprocess")
         self.px_h.copy_(self.px_d, non_blocking=True)
