@@ -187,6 +187,23 @@ typedef struct pa_traj_args {
 
 int pa_trajectory_linearize(const pa_traj_args* args, void* stream);
 
+/* Factor-graph consumer (the graph and optimizer are not in the
+ * reference -- GTSAM's LM runs on the host -- so this build defines them): one damped
+ * Gauss-Newton / LM step per trajectory from pa_trajectory_linearize's WHITENED outputs
+ * (same layouts; every Jacobian required).  Per frame the variable block is
+ * x = [pose tangent (6, [omega; v]) | angular velocity (3) | velocity (3)]; the step
+ * solves (J^T J + lambda I) delta = -J^T r.  Outputs: D (T*L, 12, 12) diagonal and
+ * E (T*(L-1), 12, 12) off-diagonal blocks of J^T J (E_l couples frame l rows with
+ * frame l+1 columns), g (T*L, 12) = J^T r, delta (T*L, 12), info (T) = 0 or the
+ * 1-based frame whose pivot block was not positive definite (delta NaN).  Projection
+ * factors with status != 0 (cheirality) are skipped.  ws: pa_trajectory_gn_workspace. */
+size_t pa_trajectory_gn_workspace(int T, int L);
+int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const double* j_proj,
+                          const int32_t* status_proj, const double* r_dyn, const double* j_dyn0,
+                          const double* j_dyn1, const double* j_dyn2, const double* j_dyn3, const double* r_cv,
+                          const double* j_cv0, const double* j_cv1, double lambda, double* D, double* E, double* g,
+                          double* delta, int32_t* info, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -130,3 +130,33 @@ def detect_and_linearize(model, x: torch.Tensor, poses, vels, angvels, corners, 
     out = linearize_trajectories(y, poses, vels, angvels, corners, K, T=T, L=L, dt=dt, H=model.H, W=model.W, **kw)
     out["y"] = y
     return out
+
+
+def gn_step(lin: dict, *, T: int, L: int, lam: float = 0.0) -> dict:
+    """One damped Gauss-Newton / LM step per trajectory on the device (SURVEY.md 8f.4,
+    pa_trajectory_gn_step) from `linearize_trajectories(...)` run with whitening sigmas and
+    Jacobians.  Returns D (T*L,12,12), E (T*(L-1),12,12), g (T*L,12), delta (T*L,12) and
+    info (T,) int32 (0 = solved).  Variable block per frame: [pose (6) | angvel (3) | vel (3)]."""
+    if lin.get("j_proj") is None:
+        raise RuntimeError("gn_step needs the Jacobians (linearize with jacobians=True)")
+    dev = lin["r_proj"].device
+    n_kp = lin["r_proj"].shape[0] // (T * L) if T * L else 0
+    m = T * max(L - 1, 0)
+
+    def e(*shape, dtype=torch.float64):
+        return torch.empty(shape, dtype=dtype, device=dev)
+
+    out = {"D": e(T * L, 12, 12), "E": e(max(m, 1), 12, 12), "g": e(T * L, 12), "delta": e(T * L, 12),
+           "info": e(T, dtype=torch.int32)}
+    L_ = _lib.lib()
+    ws = torch.empty(max(int(L_.pa_trajectory_gn_workspace(T, L)), 8), dtype=torch.uint8, device=dev)
+    p = _lib.ptr
+    with torch.cuda.device(dev):
+        _lib.check(L_.pa_trajectory_gn_step(
+            T, L, n_kp, p(lin["r_proj"]), p(lin["j_proj"]), p(lin.get("status")), p(lin["r_dyn"]), p(lin["j_dyn0"]),
+            p(lin["j_dyn1"]), p(lin["j_dyn2"]), p(lin["j_dyn3"]), p(lin["r_cv"]), p(lin["j_cv0"]), p(lin["j_cv1"]),
+            float(lam), p(out["D"]), p(out["E"]), p(out["g"]), p(out["delta"]), p(out["info"]), p(ws), ws.numel(),
+            _lib.stream_of(dev)), "pa_trajectory_gn_step")
+    out["E"] = out["E"][:m]
+    out["_ws"] = ws
+    return out
