@@ -423,12 +423,13 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
     }
     // layer1: the weight-resident persistent kernel for all four convs (variant 32
     // keeps the patch kernel for reference timing)
-    // shipped: the residual convs on the LDS-DMA variant (25.5 vs 28.5 us), the
-    // others on the register-staged one (24.3 vs 24.8 us)
+    // shipped: all four on the LDS-DMA variant (interleaved whole-forward A/B after the
+    // write-through epilogues: 172.7k vs 171.7k frames/s with the register-staged kernel on
+    // the two non-residual convs, profiles/r01f_variant_sweep.log)
     const bool l1 = a.Hout == 64 && a.Cout == 64 && a.Cin == 64;
     if (l1 && g_variant[1] == 0) {
       if (kname) *kname = "conv3x3c64_l1";
-      return (a.epi & EPI_RES) ? launch_conv3x3_c64d(a, 0, s) : launch_conv3x3_c64(a, 0, s);
+      return launch_conv3x3_c64d(a, 0, s);
     }
     const bool c64 = g_variant[1] >= 30 && g_variant[1] <= 39 && g_variant[1] != 32;
     if (l1 && c64) {
