@@ -83,9 +83,6 @@ int pa_detector_forward_rgbd(pa_detector* d, const uint8_t* rgb_dev, const float
 int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream,
                         float* ms_out, const char** names_out, int max_n);
 
-/* Tuning hook for interleaved A/B timing (tools/layer_ab.py): selects kernel
- * variant `variant` for layer 1..4 (stage) or 0 (stem); 0 = the shipped choice.
- * Process-global; not thread-safe; never needed in production. */
 /* Average device time of ONE launch of the forward (index in pa_detector_profile
  * order): the forward runs once with that launch issued `reps` times back to back
  * between two HIP events on `stream`.  y_dev and the activations are scratch
@@ -93,12 +90,6 @@ int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev,
  * using outputs.  Test/measurement entry point, not part of the drop-in surface. */
 int pa_detector_time_launch(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream, int index,
                             int reps, float* avg_ms_out, const char** name_out);
-
-int pa_debug_set_variant(int layer, int variant);
-/* Timestamping kernel variants write s_memrealtime stamps (100 MHz) to
- * trace_dev + launch * 65536 + workgroup * 64 (launch = index in the forward, stem = 0);
- * nullptr turns it off.  Measurement entry point. */
-int pa_debug_set_trace(unsigned long long* trace_dev);
 
 /* Algorithmic FLOPs of one frame's forward (2 x MAC over the 20 convs + fc). */
 double pa_detector_flops_per_frame(const pa_detector* d);

@@ -1,0 +1,29 @@
+/*
+ * perseus_amd — tuning / measurement hooks of libperseus_amd.so.  Not part of the
+ * drop-in surface (include/perseus_amd.h); nothing in production calls these.
+ * Both settings belong to one pa_detector handle and apply to that handle's
+ * forwards only (another handle in the same process keeps its own).
+ */
+#ifndef PERSEUS_AMD_DEBUG_H
+#define PERSEUS_AMD_DEBUG_H
+
+#include "perseus_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Interleaved A/B timing (tools/layer_ab.py, tools/head_ab.py): select kernel variant
+ * `variant` for layer 1..4 (stage), 0 (stem), 5-7 (stride-2 entry / head options);
+ * 0 = the shipped choice. */
+int pa_detector_debug_set_variant(pa_detector* d, int layer, int variant);
+
+/* Timestamping kernel variants write s_memrealtime stamps (100 MHz) to
+ * trace_dev + launch * 65536 + workgroup * 64 (launch = index in the forward, stem = 0);
+ * NULL turns it off. */
+int pa_detector_debug_set_trace(pa_detector* d, unsigned long long* trace_dev);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PERSEUS_AMD_DEBUG_H */

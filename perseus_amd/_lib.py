@@ -50,8 +50,8 @@ _SIGS = {
     "pa_detector_flops_per_frame": (C.c_double, [C.c_void_p]),
     "pa_detector_time_launch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                           C.c_int, C.c_void_p, C.c_void_p]),
-    "pa_debug_set_variant": (C.c_int, [C.c_int, C.c_int]),
-    "pa_debug_set_trace": (C.c_int, [C.c_void_p]),
+    "pa_detector_debug_set_variant": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "pa_detector_debug_set_trace": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pa_preprocess_rgbd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.c_float, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "pa_keypoints_postprocess": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -75,6 +75,15 @@ _SIGS = {
 
 PREC_FP16 = 0
 PREC_FP32 = 1
+PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32}
+
+
+def precision_code(name: str) -> int:
+    try:
+        return PRECISIONS[name]
+    except KeyError:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {name!r}") from None
+
 VEL_WORLD = 0
 VEL_BODY = 1
 

@@ -6,6 +6,7 @@
 #include <string>
 
 #include "../../include/perseus_amd.h"
+#include "../../include/perseus_amd_debug.h"
 
 namespace pa {
 

@@ -10,10 +10,13 @@ namespace pa {
 enum { EPI_RELU = 1, EPI_RES = 2, EPI_HEAD = 4 };
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-extern int g_variant[8];  // kernel-variant selector per layer (A/B timing; 0 = shipped)
-// pa_debug_set_trace: device buffer for the timestamping variants; launch i of a
-// forward gets g_trace + i * TRACE_LAUNCH (nullptr = off)
-extern unsigned long long* g_trace;
+// Kernel-variant selector per layer (A/B timing; 0 = shipped) and the timestamp buffer
+// of the tracing variants (launch i of a forward gets g_trace + i * TRACE_LAUNCH;
+// nullptr = off).  Both belong to a pa_detector handle (pa_detector_debug_set_variant /
+// _set_trace, include/perseus_amd_debug.h): a forward points these thread-locals at its
+// handle's settings for the duration of the call, so handles never see each other's.
+extern thread_local const int* g_variant;
+extern thread_local unsigned long long* g_trace;
 constexpr int TRACE_SLOTS = 64, TRACE_LAUNCH = 65536;
 
 // 16-byte store at byte offset `off` from the wave-uniform base `base`; WT = write-through

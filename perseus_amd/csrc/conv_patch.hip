@@ -400,9 +400,11 @@ static int run_patch(const ConvArgs& a, hipStream_t s) {
 }
 
 // Stride-1 3x3 conv, Hin == Hout.  Tile configuration per feature-map size;
-// g_variant[layer] (pa_debug_set_variant) selects alternatives for A/B timing.
-int g_variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-unsigned long long* g_trace = nullptr;
+// g_variant[layer] (the handle's pa_detector_debug_set_variant) selects alternatives
+// for A/B timing.
+static const int k_shipped_variants[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+thread_local const int* g_variant = k_shipped_variants;
+thread_local unsigned long long* g_trace = nullptr;
 
 template <typename T>
 int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {

@@ -54,6 +54,8 @@ struct pa_detector {
   int head_cap = 0;          // batch capacity of pool / cnt
   double flops_per_frame = 0;
   int device = 0;
+  int variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // pa_detector_debug_set_variant (0 = shipped)
+  unsigned long long* trace = nullptr;         // pa_detector_debug_set_trace
 };
 
 namespace pa {
@@ -395,13 +397,44 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   return PA_OK;
 }
 
+// Points the launchers' thread-local variant / trace selectors at this handle's settings
+// for one call (conv.h g_variant), restoring the previous ones on exit.
+struct HandleScope {
+  const int* v;
+  unsigned long long* t;
+  explicit HandleScope(const pa_detector* d) : v(g_variant), t(g_trace) {
+    g_variant = d->variant;
+    g_trace = d->trace;
+  }
+  ~HandleScope() {
+    g_variant = v;
+    g_trace = t;
+  }
+};
+
+// Frames per forward_t pass.  Every activation offset in the kernels is 32-bit (buffer
+// stores, 2 GB); a batch of B frames needs B * 64*64*64 * 2 bytes per fp16 map (x2 for
+// the hi/lo pair of the fp16x3 mode), so larger batches run as consecutive chunks on the
+// same stream (each chunk already fills the chip many times over).
+constexpr int kChunk = 1024;
+
 static int forward(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof) {
   PA_CHECK(d, "null detector");
   PA_CHECK(B >= 0, "batch %d", B);
   if (B == 0) return PA_OK;
   PA_CHECK(x && y, "null input/output pointer");
-  PA_TRY(ensure_ws(d, B));
-  return d->prec == PA_PREC_FP32 ? forward_t<float>(d, x, B, y, s, prof) : forward_t<_Float16>(d, x, B, y, s, prof);
+  PA_TRY(ensure_ws(d, B < kChunk ? B : kChunk));
+  HandleScope hs(d);
+  const size_t in_frame = (size_t)d->in_ch * d->H * d->W, out_frame = 2 * (size_t)d->n_kp;
+  for (int off = 0; off < B; off += kChunk) {
+    const int nb = B - off < kChunk ? B - off : kChunk;
+    const float* xc = x + off * in_frame;
+    float* yc = y + off * out_frame;
+    const int rc = d->prec == PA_PREC_FP32 ? forward_t<float>(d, xc, nb, yc, s, prof)
+                                           : forward_t<_Float16>(d, xc, nb, yc, s, prof);
+    if (rc != PA_OK) return rc;
+  }
+  return PA_OK;
 }
 
 // camera frames -> keypoints, preprocess fused into the stem (fp16, 4-channel models)
@@ -414,8 +447,18 @@ static int forward_rgbd(pa_detector* d, const RgbdSrc& src, int B, float* y, hip
                                     "pa_detector_forward)");
   PA_CHECK(d->in_ch == 4, "forward_rgbd: needs a 4-channel (RGBD) model, have %d", d->in_ch);
   PA_CHECK(src.Hs >= 256 && src.Ws >= 256, "forward_rgbd: source %dx%d smaller than 256x256", src.Hs, src.Ws);
-  PA_TRY(ensure_ws(d, B));
-  return forward_t<_Float16>(d, nullptr, B, y, s, nullptr, &src);
+  PA_TRY(ensure_ws(d, B < kChunk ? B : kChunk));
+  HandleScope hs(d);
+  const size_t frame = (size_t)src.Hs * src.Ws;
+  for (int off = 0; off < B; off += kChunk) {
+    const int nb = B - off < kChunk ? B - off : kChunk;
+    RgbdSrc c = src;
+    c.rgb = src.rgb + off * frame * 3;
+    c.depth = src.depth + off * frame;
+    const int rc = forward_t<_Float16>(d, nullptr, nb, y + off * 2 * (size_t)d->n_kp, s, nullptr, &c);
+    if (rc != PA_OK) return rc;
+  }
+  return PA_OK;
 }
 
 }  // namespace pa
@@ -551,14 +594,16 @@ int pa_detector_time_launch(pa_detector* d, const float* x_dev, int B, float* y_
   return rc;
 }
 
-int pa_debug_set_trace(unsigned long long* trace_dev) {
-  pa::g_trace = trace_dev;
+int pa_detector_debug_set_trace(pa_detector* d, unsigned long long* trace_dev) {
+  PA_CHECK(d, "null detector");
+  d->trace = trace_dev;
   return PA_OK;
 }
 
-int pa_debug_set_variant(int layer, int variant) {
+int pa_detector_debug_set_variant(pa_detector* d, int layer, int variant) {
+  PA_CHECK(d, "null detector");
   PA_CHECK(layer >= 0 && layer < 8 && variant >= 0, "layer %d variant %d", layer, variant);
-  pa::g_variant[layer] = variant;
+  d->variant[layer] = variant;
   return PA_OK;
 }
 

@@ -110,6 +110,7 @@ class KeypointCNN(nn.Module):
         self._handle = None
         self._handle_dev = None
         self._stamp = None
+        self._variants = {}
         self.eval()
 
     # -------------------------------------------------------------- weights
@@ -127,21 +128,52 @@ class KeypointCNN(nn.Module):
         parts = [sd[k].detach().to("cpu", torch.float32).reshape(-1).numpy() for k in float_keys(shapes)]
         return np.ascontiguousarray(np.concatenate(parts))
 
-    def _ensure_handle(self, device: torch.device):
-        stamp = self._fingerprint()
-        if self._handle is not None and self._stamp == stamp and self._handle_dev == device:
-            return self._handle
-        self._release()
+    def _new_handle(self, device: torch.device):
+        """A fresh pa_detector handle on `device` holding the current weights (the
+        caller owns it: pa_detector_destroy)."""
         L = _lib.lib()
         blob = self._blob()
         h = _lib.C.c_void_p()
         with torch.cuda.device(device):
             _lib.check(L.pa_detector_create(blob.ctypes.data, blob.nbytes, self.num_channels, self.n_keypoints,
                                             self.H, self.W, _lib.C.byref(h)), "pa_detector_create")
+        for layer in range(8):
+            _lib.check(L.pa_detector_debug_set_variant(h, layer, self._variants.get(layer, 0)), "set_variant")
+        return h
+
+    def _ensure_handle(self, device: torch.device):
+        stamp = self._fingerprint()
+        if self._handle is not None and self._stamp == stamp and self._handle_dev == device:
+            return self._handle
+        self._release()
+        h = self._new_handle(device)
         self._handle = h
         self._handle_dev = device
         self._stamp = stamp
         return h
+
+    def refresh_weights(self) -> None:
+        """Re-upload the weights on the next forward.  Needed only after writes that
+        bypass the version counters the fingerprint reads (`param.data[...] = v`,
+        `param.data.copy_(v)`); load_state_dict and in-place ops on the parameters
+        themselves are picked up automatically."""
+        self._stamp = None
+
+    def set_variants(self, variants: "dict[int, int] | None" = None) -> None:
+        """Tuning hook (include/perseus_amd_debug.h): kernel variant per layer for THIS
+        model's handle; {} / None restores the shipped kernels."""
+        self._variants = dict(variants or {})
+        if self._handle is not None:
+            L = _lib.lib()
+            for layer in range(8):
+                _lib.check(L.pa_detector_debug_set_variant(self._handle, layer, self._variants.get(layer, 0)),
+                           "set_variant")
+
+    def set_trace(self, trace: "torch.Tensor | None") -> None:
+        """Timestamp buffer of the tracing kernel variants (None = off)."""
+        dev = trace.device if trace is not None else torch.device("cuda", torch.cuda.current_device())
+        _lib.check(_lib.lib().pa_detector_debug_set_trace(self._ensure_handle(dev),
+                                                           None if trace is None else trace.data_ptr()), "set_trace")
 
     def _release(self):
         if self._handle is not None:
@@ -188,7 +220,7 @@ class KeypointCNN(nn.Module):
         dev = x.device
         h = self._ensure_handle(dev)
         L = _lib.lib()
-        _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP32 if self.precision == "fp32" else _lib.PREC_FP16),
+        _lib.check(L.pa_detector_set_precision(h, _lib.precision_code(self.precision)),
                    "set_precision")
         shape = (x.shape[0], 2 * self.n_keypoints)
         if out is not None:
@@ -238,7 +270,7 @@ class KeypointCNN(nn.Module):
         dev = x.device
         h = self._ensure_handle(dev)
         L = _lib.lib()
-        _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP32 if self.precision == "fp32" else _lib.PREC_FP16),
+        _lib.check(L.pa_detector_set_precision(h, _lib.precision_code(self.precision)),
                    "set_precision")
         y = torch.full((x.shape[0], 2 * self.n_keypoints), float("nan"), dtype=torch.float32, device=dev)
         ms = (_lib.C.c_float * max_kernels)()
@@ -256,7 +288,7 @@ class KeypointCNN(nn.Module):
         dev = x.device
         h = self._ensure_handle(dev)
         L = _lib.lib()
-        _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP32 if self.precision == "fp32" else _lib.PREC_FP16),
+        _lib.check(L.pa_detector_set_precision(h, _lib.precision_code(self.precision)),
                    "set_precision")
         y = torch.empty((x.shape[0], 2 * self.n_keypoints), dtype=torch.float32, device=dev)
         ms = _lib.C.c_float()

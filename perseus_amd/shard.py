@@ -32,13 +32,15 @@ def trajectory_range(n_traj: int, traj_len: int, world: int, rank: int) -> tuple
     return t0 * traj_len, t1 * traj_len
 
 
-def gather_keypoints(y_local: torch.Tensor, group=None) -> torch.Tensor:
+def gather_keypoints(y_local: torch.Tensor, group=None, force: bool = False) -> torch.Tensor:
     """All-gather (n_i, D) blocks of every rank -> (sum n_i, D), rank order.
 
     Shard sizes may differ (frame_range): counts are exchanged first (one tiny
     all_gather), blocks are padded to the largest and trimmed after the single
-    data all_gather.  On device tensors with the nccl backend this is RCCL."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    data all_gather.  On device tensors with the nccl backend this is RCCL.  A
+    single-rank group returns y_local unless `force` (tests run the collective path
+    at world size 1, the most one GPU can host)."""
+    if not dist.is_initialized() or (dist.get_world_size(group) == 1 and not force):
         return y_local
     world = dist.get_world_size(group)
     y_local = y_local.contiguous()

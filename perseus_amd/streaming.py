@@ -52,11 +52,14 @@ class StreamingPipeline:
         self.y = torch.empty((n, 2 * K), dtype=torch.float32, device=self.dev)
         self.px_d = torch.empty((n, K, 2), dtype=torch.float32, device=self.dev)
         self.stream = torch.cuda.Stream(self.dev)
-        model.reserve(n, self.dev)
-        self._h = model._ensure_handle(self.dev)
+        # A private handle: the captured graph holds its weight and workspace pointers, so
+        # nothing the model does later (a larger batch growing its workspace, a weight
+        # reload destroying its handle) may free them under the graph.  Weights are taken
+        # as of construction.
         L = _lib.lib()
-        _lib.check(L.pa_detector_set_precision(self._h, _lib.PREC_FP32 if model.precision == "fp32"
-                                               else _lib.PREC_FP16), "set_precision")
+        self._h = model._new_handle(self.dev)
+        _lib.check(L.pa_detector_set_precision(self._h, _lib.precision_code(model.precision)), "set_precision")
+        _lib.check(L.pa_detector_reserve(self._h, n), "reserve")
         if model.num_channels != 4:
             raise ValueError("StreamingPipeline feeds RGBD (num_channels=4)")
         self.graph = None
@@ -114,3 +117,17 @@ class StreamingPipeline:
     def __call__(self, rgb: np.ndarray, depth: np.ndarray) -> np.ndarray:
         self.stage(rgb, depth)
         return self.run()
+
+    def close(self) -> None:
+        """Drop the graph, then the handle it captured."""
+        self.graph = None
+        if getattr(self, "_h", None) is not None:
+            torch.cuda.synchronize(self.dev)
+            _lib.lib().pa_detector_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

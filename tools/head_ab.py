@@ -37,8 +37,7 @@ def main():
     with torch.no_grad():
         for _ in range(a.rounds):
             for name, vs in variants:
-                for layer, v in vs:
-                    _lib.check(L.pa_debug_set_variant(layer, v))
+                m.set_variants(dict(vs))
                 for _ in range(20):
                     m(x, out=out)
                 torch.cuda.synchronize()
@@ -47,8 +46,7 @@ def main():
                     m(x, out=out)
                 torch.cuda.synchronize()
                 res[name].append(64 * a.steps / (time.perf_counter() - t0))
-                for layer in range(8):
-                    L.pa_debug_set_variant(layer, 0)
+                m.set_variants({})
     for k, v in res.items():
         print(json.dumps({"variant": k, "frames_per_s_median": float(np.median(v)), "runs": [round(u) for u in v]}),
               flush=True)

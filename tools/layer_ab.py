@@ -38,8 +38,7 @@ def main():
     res = {}
     for r in range(a.rounds + 1):
         for v in a.variants:
-            for layer in a.layers:
-                _lib.check(L.pa_debug_set_variant(layer, v))
+            m.set_variants({layer: v for layer in a.layers})
             if r == 0:
                 y = m(x)
                 if ref is None:
@@ -61,8 +60,7 @@ def main():
             line += f" | v{v} {med*1e3:6.1f} ({min(t)*1e3:5.1f})"
         print(line)
     print("total " + " | ".join(f"v{v} {tot[v]*1e3:.1f}us" for v in a.variants))
-    for layer in a.layers:
-        L.pa_debug_set_variant(layer, 0)
+    m.set_variants({})
 
 
 if __name__ == "__main__":

@@ -20,7 +20,7 @@ def main():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--precision", default="fp16")
     p.add_argument("--out", required=True)
-    p.add_argument("--variant", action="append", default=[], help="LAYER:VARIANT (pa_debug_set_variant)")
+    p.add_argument("--variant", action="append", default=[], help="LAYER:VARIANT (pa_detector_debug_set_variant)")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -28,13 +28,10 @@ def main():
     from perseus_amd import _lib, synth
     from perseus_amd.detector import KeypointCNN
 
-    for lv in a.variant:
-        layer, v = (int(t) for t in lv.split(":"))
-        _lib.check(_lib.lib().pa_debug_set_variant(layer, v))
-
     dev = torch.device("cuda", 0)
     m = KeypointCNN(num_channels=4, precision=a.precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
+    m.set_variants(dict(tuple(int(t) for t in lv.split(":")) for lv in a.variant))
     x = torch.from_numpy(synth.synthetic_frames(0, a.batch)).to(dev)
     m.reserve(a.batch, dev)
     with torch.no_grad():
@@ -46,7 +43,9 @@ def main():
     torch.cuda.synchronize()
     os.makedirs(a.out, exist_ok=True)
     with open(os.path.join(a.out, "names.json"), "w") as fh:
-        json.dump({"batch": a.batch, "precision": a.precision, "names": names,
+        from bench import csrc_digest
+
+        json.dump({"batch": a.batch, "precision": a.precision, "names": names, "csrc": csrc_digest(),
                    "forwards": a.warmup + a.iters + 1}, fh)
     print(f"{a.warmup + a.iters + 1} forwards x {len(names)} launches, B={a.batch}")
 

@@ -150,7 +150,8 @@ def main():
         tf = os.path.join(out, "pmc_traffic.json")
         allt = json.load(open(tf)) if os.path.exists(tf) else {}
         allt = {k: v for k, v in allt.items() if isinstance(v, dict) and "bytes_per_launch" in v}
-        allt[prec] = {"batch": B, "names": names, "bytes_per_launch": [round(f + w) for f, w in zip(fb, wb)],
+        allt[prec] = {"batch": B, "names": names, "csrc": meta.get("csrc"), "symbols": syms,
+                      "bytes_per_launch": [round(f + w) for f, w in zip(fb, wb)],
                       "fetch_bytes": [round(f) for f in fb], "write_bytes": [round(w) for w in wb],
                       "source": f"profiles/{a.tag}_summary.md: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE "
                                 f"(separate passes) over tools/pmc_forward.py, FETCH x2 (gfx950), median over forwards"}

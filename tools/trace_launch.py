@@ -1,5 +1,5 @@
 """Per-workgroup phase timeline of one forward launch from a timestamping kernel
-variant (pa_debug_set_trace; conv.h trace_stamp, s_memrealtime = 100 MHz).
+variant (pa_detector_debug_set_trace; conv.h trace_stamp, s_memrealtime = 100 MHz).
 
     python tools/trace_launch.py --layer 1 --variant 36 --launch 1 2 3 4
 
@@ -32,16 +32,14 @@ def main():
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
     x = torch.from_numpy(synth.synthetic_frames(0, a.batch)).cuda()
     buf = torch.zeros(24 * 65536, dtype=torch.int64, device="cuda")
-    for layer in a.layer:
-        _lib.check(L.pa_debug_set_variant(layer, a.variant))
-    _lib.check(L.pa_debug_set_trace(buf.data_ptr()))
+    m.set_variants({layer: a.variant for layer in a.layer})
+    m.set_trace(buf)
     for _ in range(a.runs):
         buf.zero_()
         m(x)
         torch.cuda.synchronize()
-    _lib.check(L.pa_debug_set_trace(None))
-    for layer in a.layer:
-        L.pa_debug_set_variant(layer, 0)
+    m.set_trace(None)
+    m.set_variants({})
     t = buf.view(24, -1, 64).cpu().numpy()
     for li in a.launch:
         tl = t[li]
