@@ -30,8 +30,10 @@ extern "C" {
 #define PA_EHIP -2     /* HIP runtime error (message has hipGetErrorString)   */
 #define PA_ENOMEM -3   /* device allocation failed                            */
 
-#define PA_PREC_FP16 0 /* fp16 NHWC activations/weights, fp32 MFMA accumulate */
-#define PA_PREC_FP32 1 /* fp32 NHWC, exact-f32 MFMA (parity mode)             */
+#define PA_PREC_FP16 0   /* fp16 NHWC activations/weights, fp32 MFMA accumulate     */
+#define PA_PREC_FP32 1   /* fp32 NHWC, exact-f32 MFMA (reference parity mode)     */
+#define PA_PREC_FP16X3 2 /* fast parity mode: hi/lo fp16 planes, 3 fp16 MFMA products
+                            per MAC (x_hi w_hi + x_lo w_hi + x_hi w_lo), f32 accumulate */
 
 #define PA_VEL_WORLD 0 /* factors.py:41 vel_frame="world" */
 #define PA_VEL_BODY 1  /* vel_frame="body"                */
@@ -60,7 +62,7 @@ void pa_detector_destroy(pa_detector* d);
  * captured graph). */
 int pa_detector_reserve(pa_detector* d, int max_batch);
 
-/* PA_PREC_FP16 (default) or PA_PREC_FP32. */
+/* PA_PREC_FP16 (default), PA_PREC_FP32 or PA_PREC_FP16X3. */
 int pa_detector_set_precision(pa_detector* d, int precision);
 
 /* Replaces KeypointCNN.forward (models.py:34-40): x (B,C,H,W) f32 NCHW contiguous

@@ -75,7 +75,8 @@ _SIGS = {
 
 PREC_FP16 = 0
 PREC_FP32 = 1
-PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32}
+PREC_FP16X3 = 2
+PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16x3": PREC_FP16X3}
 
 
 def precision_code(name: str) -> int:

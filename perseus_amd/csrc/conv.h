@@ -41,6 +41,7 @@ struct ConvArgs {
   const void* in;     // NHWC [B][Hin][Win][Cin]
   const void* w;      // [Cout][KS][KS][Cin], BatchNorm folded
   const float* bias;  // [Cout], BatchNorm folded
+  const float* scale; // fp16x3 only: [Cout] 2^-e, unscales the accumulator (weights hold w * 2^e)
   const void* res;    // NHWC [B][Hout][Wout][Cout] or nullptr
   void* out;          // NHWC [B][Hout][Wout][Cout]
   int B, Hin, Win, Cin, Hout, Wout, Cout, stride, pad, epi, M;
@@ -61,6 +62,8 @@ struct ConvS2Args {
   const float* bias;   // [Cout]
   const void* wds;     // [Cout][Cin]
   const float* bias2;  // [Cout]
+  const float* scale;  // fp16x3 only: [Cout] 2^-e of w / wds
+  const float* scale2;
   void* out;           // NHWC [B][Hout][Wout][Cout]
   void* out2;          // NHWC [B][Hout][Wout][Cout]
   int B, Hin, Win, Cin, Hout, Wout, Cout;
@@ -108,6 +111,18 @@ int launch_stem_pool_rgbd(const RgbdSrc& src, int B, const _Float16* w, const fl
                           hipStream_t s);
 int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out,
                           hipStream_t s);
+
+// fp16x3 parity mode (stem_x3.hip, conv_x3_*.hip, conv.hip head_x3): activations are
+// [hi (C) | lo (C)] fp16 plane pairs per pixel, weights hi/lo planes of w * 2^e
+int launch_stem_pool_x3(const float* x, int B, int Cin, const _Float16* w, const float* bias_s, const float* scale,
+                        _Float16* out, hipStream_t s);
+int launch_conv3x3_x3_l1(const ConvArgs& a, hipStream_t s);
+int launch_conv3x3_x3_l2(const ConvArgs& a, hipStream_t s);
+int launch_conv3x3_x3_l3(const ConvArgs& a, hipStream_t s);
+int launch_conv3x3_x3_l4(const ConvArgs& a, hipStream_t s);
+int launch_conv3x3s2_x3(const ConvS2Args& a, hipStream_t s, const char** kname);
+int launch_head_x3(const _Float16* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
+                   hipStream_t s);
 
 template <typename T>
 int launch_maxpool(const T* in, int B, int H, int W, int C, T* out, hipStream_t s);

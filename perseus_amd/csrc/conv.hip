@@ -561,6 +561,69 @@ __global__ __launch_bounds__(256) void head_fp16(const _Float16* __restrict__ in
   if (tid < NOUT) y[(size_t)n * NOUT + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + fcb[tid];
 }
 
+// fp16x3 parity mode: head_fp16's arithmetic on the f32 values hi + lo of the layer4
+// output's plane pair ([hi (512) | lo (512)] per pixel; hi + lo is exact in f32).
+template <int NOUT>
+__global__ __launch_bounds__(256) void head_x3(const _Float16* __restrict__ in, const float* __restrict__ fcw,
+                                               const float* __restrict__ fcb, float* __restrict__ y) {
+  constexpr int HW = 64, C = 512;
+  __shared__ float csum[4][C];
+  __shared__ float part[4][NOUT];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = tid >> 6, c8 = tid & 63;
+  const _Float16* p = in + (size_t)n * HW * 2 * C + c8 * 8;
+  half8 h[HW / 4], l[HW / 4];
+#pragma unroll
+  for (int u = 0; u < HW / 4; ++u) {
+    h[u] = *reinterpret_cast<const half8*>(p + (size_t)(g + 4 * u) * 2 * C);
+    l[u] = *reinterpret_cast<const half8*>(p + (size_t)(g + 4 * u) * 2 * C + C);
+  }
+  const int c = 2 * tid;
+  float fw[NOUT][2];
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    const float2 v = *reinterpret_cast<const float2*>(fcw + (size_t)j * C + c);
+    fw[j][0] = v.x;
+    fw[j][1] = v.y;
+  }
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < HW / 4; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += (float)h[u][e] + (float)l[u][e];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) csum[g][c8 * 8 + e] = s[e];
+  __syncthreads();
+  const float inv = 1.0f / (float)HW;
+  const float m0 = (csum[0][c] + csum[1][c] + csum[2][c] + csum[3][c]) * inv;
+  const float m1 = (csum[0][c + 1] + csum[1][c + 1] + csum[2][c + 1] + csum[3][c + 1]) * inv;
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    float v = fmaf(fw[j][1], m1, fw[j][0] * m0);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) part[wid][j] = v;
+  }
+  __syncthreads();
+  if (tid < NOUT) y[(size_t)n * NOUT + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + fcb[tid];
+}
+
+int launch_head_x3(const _Float16* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
+                   hipStream_t s) {
+  PA_CHECK(HW == 64 && C == 512 && nout >= 1 && nout <= 32, "head x3: HW=%d C=%d nout=%d", HW, C, nout);
+  if (B <= 0) return PA_OK;
+  switch (nout) {
+#define PA_HX3(N) \
+  case N: hipLaunchKernelGGL(head_x3<N>, dim3(B), dim3(256), 0, s, in, fcw, fcb, y); break;
+    PA_HX3(2) PA_HX3(4) PA_HX3(6) PA_HX3(8) PA_HX3(10) PA_HX3(12) PA_HX3(14) PA_HX3(16) PA_HX3(18) PA_HX3(20)
+    PA_HX3(22) PA_HX3(24) PA_HX3(26) PA_HX3(28) PA_HX3(30) PA_HX3(32)
+#undef PA_HX3
+    default: PA_CHECK(false, "head x3: nout %d (2 * n_keypoints)", nout);
+  }
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
 template <typename T>
 int launch_head(const T* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
                 hipStream_t s) {

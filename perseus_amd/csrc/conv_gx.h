@@ -25,6 +25,14 @@
 // W(s + PD), at the first group start of a block the next block's patch, RSD steps before the end the bias
 // (+ residual) loads; MFMAs of 2s+1; wait for what step s + 2's fragments need and
 // cross a bare s_barrier.
+//
+// X3 (the fp16x3 parity mode): activations are a pair of fp16 planes per
+// pixel, [hi (Cin) | lo (Cin)] with hi = fp16(v), lo = fp16(v - hi), and the weights
+// [tap][hi (Cin) | lo (Cin)] of w * 2^e_co (e_co per output channel, so lo stays a
+// normal fp16).  Each 64-channel block becomes 3 virtual blocks with the products
+// x_hi w_hi, x_hi w_lo, x_lo w_hi accumulated in f32 (x_lo w_lo, below 2^-22 relative, is
+// dropped); the epilogue unscales by 2^-e_co exactly and writes the result as a new
+// (hi, lo) pair.  The K loop machinery is the same, with 3x the steps.
 #pragma once
 #include <type_traits>
 
@@ -217,13 +225,35 @@ __device__ __forceinline__ void gx_head(const ConvArgs& a, char* smem, const f32
 // 2 = also no weight / patch DMAs in the K loop, 3 = no K loop (prologue + epilogue);
 // 4 = the shipped kernel plus s_memrealtime stamps into a.trace (conv.h trace_stamp)
 // FD: fragment reads run FD half-steps ahead of the MFMAs (FD + 1 register sets)
+// X3 virtual block vb of a CIN = 64 * NCB conv: the 64-channel block of the activation
+// planes [hi | lo] (pblk) and of the weight planes (wblk) it multiplies
+template <bool X3, int NCB>
+struct GxBlocks {
+  static constexpr int NVB = X3 ? 3 * NCB : NCB;
+  static constexpr int pblk(int vb) { return X3 ? (vb % 3 == 2 ? NCB + vb / 3 : vb / 3) : vb; }
+  static constexpr int wblk(int vb) { return X3 ? (vb % 3 == 1 ? NCB + vb / 3 : vb / 3) : vb; }
+};
+
+// hi / lo fp16 pair of an f32 value (hi + lo == v to 2^-22 relative)
+struct HiLo {
+  _Float16 hi, lo;
+};
+__device__ __forceinline__ HiLo split_x3(float v) {
+  const _Float16 h = (_Float16)v;
+  return HiLo{h, (_Float16)(v - (float)h)};
+}
+
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1,
-          bool WT = true>
+          bool WT = true, bool X3 = false>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
-  constexpr int NSTEPS = NCB * 9;
-  constexpr int KTOT = 9 * CIN;
+  using VB = GxBlocks<X3, NCB>;
+  constexpr int XS = X3 ? 2 : 1;  // fp16 planes per activation / weight element
+  constexpr int NSTEPS = VB::NVB * 9;
+  constexpr int KW = XS * CIN;  // weight elements per tap
+  constexpr int KTOT = 9 * KW;
+  static_assert(!(X3 && (EPI & EPI_HEAD)), "fused head: fp16 path only");
   constexpr int PH = TH + 2, PW = TW + 2;
   constexpr int IMS = (TW == 8) ? ((PH * PW + 7) / 16 * 16 + 8) : PH * PW;
   constexpr int NP = NI * IMS;
@@ -242,11 +272,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   // slot (t + PD) % NSLOT, written at step t, was last read by step t + PD - NSLOT,
   // which must lie before the last barrier: t - G with a barrier every G steps
   constexpr int NSLOT = PD + G;
-  constexpr int RL = TN + ((EPI & EPI_RES) ? TM * TN / 2 : 0);
+  constexpr int RL = XS * TN + ((EPI & EPI_RES) ? XS * TM * TN / 2 : 0);
   // epilogue loads (bias, residual) issued RSD steps before the end: early enough to
   // land, late enough not to hold their VGPRs across the whole K loop
   constexpr int RSD = 4;
-  constexpr GxPlan plan{NSTEPS, NCB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G};
+  constexpr GxPlan plan{NSTEPS, VB::NVB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G};
   __shared__ __attribute__((aligned(1024))) char smem[2 * PATCHB + NSLOT * WB];
   char* patch = smem;
   char* wring = smem + 2 * PATCHB;
@@ -287,12 +317,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     const int pr = pp / PW, pcl = pp - (pp / PW) * PW;
     const int n = img0 + img, h = th0 + pr - 1, x = tw0 + pcl - 1;
     const bool ok = p < NP && pr < PH && n < a.B && (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W;
-    psrc[i] = ok ? (const char*)(in + (((size_t)n * H + h) * W + x) * CIN + lc * 8) : nullptr;
+    psrc[i] = ok ? (const char*)(in + (((size_t)n * H + h) * W + x) * KW + lc * 8) : nullptr;
   }
-  auto dma_patch = [&](int cb, int buf) __attribute__((always_inline)) {
+  auto dma_patch = [&](int vb, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PDMA; ++i) {
-      const char* s = psrc[i] ? psrc[i] + cb * 128 : (const char*)gx_zero_line;
+      const char* s = psrc[i] ? psrc[i] + VB::pblk(vb) * 128 : (const char*)gx_zero_line;
       xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
     }
   };
@@ -304,10 +334,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     wsrc[i] = w + (size_t)(n0 + xperm(co)) * KTOT + lc * 8;
   }
   auto dma_w = [&](int s) __attribute__((always_inline)) {
-    const int cb = s / 9, tap = s % 9;
+    const int vb = s / 9, tap = s % 9;
 #pragma unroll
     for (int i = 0; i < WDMA; ++i)
-      xdma16(wsrc[i] + tap * CIN + cb * 64, wring + (s % NSLOT) * WB + (i * NW + wid) * 1024);
+      xdma16(wsrc[i] + tap * KW + VB::wblk(vb) * 64, wring + (s % NSLOT) * WB + (i * NW + wid) * 1024);
   };
 
   const int o = xfrag(r16);
@@ -341,19 +371,27 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     }
     const int n = img0 + img;
     ok[tm] = n < a.B;
-    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * Cout + n0 + wn * WTN + q * 8;
+    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
   }
   half8 rv[TM][TN / 2];
+  half8 rl[X3 ? TM : 1][TN / 2];  // X3: the residual's lo plane
   f32x4 bias[TN];
+  f32x4 scl[X3 ? TN : 1];  // X3: 2^-e per output channel
   auto load_epi = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-      bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + n0 + wn * WTN + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4);
+    for (int tn = 0; tn < TN; ++tn) {
+      const int c = n0 + wn * WTN + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4;
+      bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + c);
+      if constexpr (X3) scl[tn] = *reinterpret_cast<const f32x4*>(a.scale + c);
+    }
     if constexpr (EPI & EPI_RES) {
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-        for (int p = 0; p < TN / 2; ++p) rv[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + p * 32);
+        for (int p = 0; p < TN / 2; ++p) {
+          rv[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + p * 32);
+          if constexpr (X3) rl[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + Cout + p * 32);
+        }
     }
   };
 
@@ -414,7 +452,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     // DMAs after this step's LDS reads (they are issued by then; see xdma16)
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + PD < NSTEPS && DBG < 2) dma_w(S + PD);
-    if constexpr (CB + 1 < NCB && S == plan.ps(CB + 1) && DBG < 2) dma_patch(CB + 1, (CB + 1) & 1);
+    if constexpr (CB + 1 < VB::NVB && S == plan.ps(CB + 1) && DBG < 2) dma_patch(CB + 1, (CB + 1) & 1);
     if constexpr (S == plan.rs) {
       // vm_after() counts these after this step's DMAs: keep the scheduler from
       // moving the (read-only) loads across them
@@ -446,14 +484,24 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     if (!ok[tm]) continue;
 #pragma unroll
     for (int p = 0; p < TN / 2; ++p) {
-      half8 hv;
+      half8 hv, lv;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float v = acc[tm][2 * p + (j >> 2)][j & 3] + bias[2 * p + (j >> 2)][j & 3];
-        if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
-        hv[j] = (_Float16)fmaxf(v, 0.f);
+        const int tn = 2 * p + (j >> 2), e = j & 3;
+        if constexpr (X3) {
+          float v = acc[tm][tn][e] * scl[tn][e] + bias[tn][e];  // exact unscale (power of 2)
+          if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j] + (float)rl[tm][p][j];
+          const HiLo hl = split_x3(fmaxf(v, 0.f));
+          hv[j] = hl.hi;
+          lv[j] = hl.lo;
+        } else {
+          float v = acc[tm][tn][e] + bias[tn][e];
+          if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
+          hv[j] = (_Float16)fmaxf(v, 0.f);
+        }
       }
       store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), hv);
+      if constexpr (X3) store16<WT>(out, (unsigned)((pixo[tm] + Cout + p * 32) * 2), lv);
     }
   }
   if constexpr (DBG == 4) {
@@ -464,7 +512,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
 }
 
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1,
-          bool WT = true>
+          bool WT = true, bool X3 = false>
 static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES) || a.epi == (EPI_RELU | EPI_RES | EPI_HEAD),
            "gx conv: epilogue %d", a.epi);
@@ -475,9 +523,10 @@ static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
   const int nsp = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW);
   const int tiles = nsp * ntn;
   const int x = xg && nsp % 8 == 0;  // whole groups of 8 spatial tiles only
-  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 < 0x7fffffffu, "gx conv: output over 2 GB");
+  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "gx conv: output over 2 GB");
+  PA_CHECK(!X3 || (a.scale && !(a.epi & EPI_HEAD)), "gx conv (fp16x3): scale required, no fused head");
   if (a.epi & EPI_HEAD) {
-    if constexpr (TH == 8 && TW == 8 && NI == 2 && BN == 64 && WM * WN == 8 && DBG == 0) {
+    if constexpr (TH == 8 && TW == 8 && NI == 2 && BN == 64 && WM * WN == 8 && DBG == 0 && !X3) {
       PA_CHECK(a.pool && a.cnt && a.fcw && a.fcb && a.y && a.Cout == 512, "gx conv: fused head arguments");
       hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES | EPI_HEAD, DBG, FD, WT>),
                          dim3(tiles), dim3(WM * WN * 64), 0, s, a, x);
@@ -485,11 +534,11 @@ static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
       PA_CHECK(false, "gx conv: fused head needs the 2 x 8x8 x 64-channel tile");
     }
   } else if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT>), dim3(tiles),
-                       dim3(WM * WN * 64), 0, s, a, x);
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT, X3>),
+                       dim3(tiles), dim3(WM * WN * 64), 0, s, a, x);
   else
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT>), dim3(tiles), dim3(WM * WN * 64), 0, s,
-                       a, x);
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT, X3>), dim3(tiles),
+                       dim3(WM * WN * 64), 0, s, a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -16,25 +16,32 @@
 // zero line.  Output pixels are row-major over the TH x TW tile (16-pixel MFMA
 // fragment = one row at TW = 16, two rows at TW = 8; for TW = 8 the row pitch is
 // padded to 20 positions so the two rows of a fragment fall on disjoint banks).
+//
+// X3 (fp16x3 parity mode): activation / weight hi-lo planes and 3 virtual blocks per
+// 64-channel block, as conv_gx.h's X3; the downsample's weights carry their own
+// per-channel power-of-2 scale (scale2).
 #pragma once
 #include "conv_gx.h"
 
 namespace pa {
 
-template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G, bool WT = true>
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G, bool WT = true, bool X3 = false>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
+  using VB = GxBlocks<X3, NCB>;
+  constexpr int XS = X3 ? 2 : 1;
   constexpr int SPB = 10;  // 9 taps + downsample per 64-channel block
-  constexpr int NSTEPS = NCB * SPB;
-  constexpr int KTOT = 9 * CIN;
+  constexpr int NSTEPS = VB::NVB * SPB;
+  constexpr int KW = XS * CIN;
+  constexpr int KTOT = 9 * KW;
   constexpr int PH = 2 * TH + 1;
   constexpr int PW = TW == 8 ? 20 : 2 * TW + 1;  // LDS positions per patch row
   constexpr int NP = PH * PW;
   constexpr int NPC = (NP * 8 + 63) / 64 * 64;
   constexpr int PDMA = NPC / 64 / NW + (NPC / 64 % NW ? 1 : 0);
   constexpr int PATCHB = (PDMA * NW * 64) * 16;
-  constexpr int NPB = NCB > 1 ? 2 : 1;  // patch buffers
+  constexpr int NPB = VB::NVB > 1 ? 2 : 1;  // patch buffers
   constexpr int WB = BN * 128;
   constexpr int WDMA = BN * 8 / NT;
   constexpr int BM = TH * TW;
@@ -45,9 +52,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile");
   static_assert(G >= 1 && G <= 3 && PD >= G + 1 && PD <= 8, "prefetch distance / steps per barrier");
   constexpr int NSLOT = PD + G;
-  constexpr int RL = 2 * TN;  // epilogue loads: bias, bias2
+  constexpr int RL = 2 * XS * TN;  // epilogue loads: bias, bias2 (+ scale, scale2)
   constexpr int RSD = 4;
-  constexpr GxPlan plan{NSTEPS, NCB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, SPB};
+  constexpr GxPlan plan{NSTEPS, VB::NVB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, SPB};
   static_assert(NPB * PATCHB + NSLOT * WB <= 163840, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[NPB * PATCHB + NSLOT * WB];
   char* patch = smem;
@@ -89,12 +96,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     const int col = pos <= TW ? 2 * pos : 2 * (pos - TW - 1) + 1;
     const int h = 2 * th0 - 1 + pr, x = 2 * tw0 - 1 + col;
     const bool ok = p < NP && pos < 2 * TW + 1 && img < a.B && (unsigned)h < (unsigned)Hin && (unsigned)x < (unsigned)Win;
-    psrc[i] = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * CIN + lc * 8) : nullptr;
+    psrc[i] = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * KW + lc * 8) : nullptr;
   }
-  auto dma_patch = [&](int cb, int buf) __attribute__((always_inline)) {
+  auto dma_patch = [&](int vb, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PDMA; ++i) {
-      const char* s = psrc[i] ? psrc[i] + cb * 128 : (const char*)gx_zero_line;
+      const char* s = psrc[i] ? psrc[i] + VB::pblk(vb) * 128 : (const char*)gx_zero_line;
       xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
     }
   };
@@ -106,13 +113,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     const int c = (i * NW + wid) * 64 + lane;
     const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
     wsrc[i] = w + (size_t)(n0 + xperm(co)) * KTOT + lc * 8;
-    dsrc[i] = wds + (size_t)(n0 + xperm(co)) * CIN + lc * 8;
+    dsrc[i] = wds + (size_t)(n0 + xperm(co)) * KW + lc * 8;
   }
   auto dma_w = [&](int s) __attribute__((always_inline)) {
-    const int cb = s / SPB, t = s % SPB;
+    const int vb = s / SPB, t = s % SPB;
+    const int wb = VB::wblk(vb) * 64;
 #pragma unroll
     for (int i = 0; i < WDMA; ++i) {
-      const _Float16* src = t < 9 ? wsrc[i] + t * CIN + cb * 64 : dsrc[i] + cb * 64;
+      const _Float16* src = t < 9 ? wsrc[i] + t * KW + wb : dsrc[i] + wb;
       xdma16(src, wring + (s % NSLOT) * WB + (i * NW + wid) * 1024);
     }
   };
@@ -125,15 +133,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     const int m = wm * WTM + tm * 16 + o;
     const int y = m / TW, x = m - (m / TW) * TW;
     ppix[tm] = 2 * y * PW + x;
-    pixo[tm] = (((size_t)(img < a.B ? img : 0) * H + th0 + y) * W + tw0 + x) * Cout + n0 + wn * WTN + q * 8;
+    pixo[tm] = (((size_t)(img < a.B ? img : 0) * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
   }
   f32x4 bias[TN], bias2[TN];
+  f32x4 scl[X3 ? TN : 1], scl2[X3 ? TN : 1];
   auto load_epi = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       const int c = n0 + wn * WTN + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4;
       bias[tn] = *reinterpret_cast<const f32x4*>(a.bias + c);
       bias2[tn] = *reinterpret_cast<const f32x4*>(a.bias2 + c);
+      if constexpr (X3) {
+        scl[tn] = *reinterpret_cast<const f32x4*>(a.scale + c);
+        scl2[tn] = *reinterpret_cast<const f32x4*>(a.scale2 + c);
+      }
     }
   };
 
@@ -193,7 +206,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     // DMAs after this step's LDS reads (see xdma16); order = GxPlan's
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + PD < NSTEPS) dma_w(S + PD);
-    if constexpr (CB + 1 < NCB && S == plan.ps(CB + 1)) dma_patch(CB + 1, (CB + 1) & 1);
+    if constexpr (CB + 1 < VB::NVB && S == plan.ps(CB + 1)) dma_patch(CB + 1, (CB + 1) & 1);
     if constexpr (S == plan.rs) {
       __builtin_amdgcn_sched_barrier(0);
       load_epi();
@@ -217,21 +230,35 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
     for (int p = 0; p < TN / 2; ++p) {
-      half8 h1, h2;
+      half8 h1, h2, l1, l2;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int tn = 2 * p + (j >> 2), e = j & 3;
-        h1[j] = (_Float16)fmaxf(acc[tm][tn][e] + bias[tn][e], 0.f);
-        h2[j] = (_Float16)(accd[tm][tn][e] + bias2[tn][e]);
+        if constexpr (X3) {
+          const HiLo a1 = split_x3(fmaxf(acc[tm][tn][e] * scl[tn][e] + bias[tn][e], 0.f));
+          const HiLo a2 = split_x3(accd[tm][tn][e] * scl2[tn][e] + bias2[tn][e]);
+          h1[j] = a1.hi;
+          l1[j] = a1.lo;
+          h2[j] = a2.hi;
+          l2[j] = a2.lo;
+        } else {
+          h1[j] = (_Float16)fmaxf(acc[tm][tn][e] + bias[tn][e], 0.f);
+          h2[j] = (_Float16)(accd[tm][tn][e] + bias2[tn][e]);
+        }
       }
       store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), h1);
       store16<WT>(out2, (unsigned)((pixo[tm] + p * 32) * 2), h2);
+      if constexpr (X3) {
+        store16<WT>(out, (unsigned)((pixo[tm] + Cout + p * 32) * 2), l1);
+        store16<WT>(out2, (unsigned)((pixo[tm] + Cout + p * 32) * 2), l2);
+      }
     }
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1, bool WT = true>
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1, bool WT = true, bool X3 = false>
 static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
-  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 < 0x7fffffffu, "s2x conv: output over 2 GB");
+  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "s2x conv: output over 2 GB");
+  PA_CHECK(!X3 || (a.scale && a.scale2), "s2x conv (fp16x3): scales required");
   PA_CHECK(a.Cin == CIN, "s2x conv: Cin %d != %d", a.Cin, CIN);
   PA_CHECK(a.Hin == 2 * a.Hout && a.Win == 2 * a.Wout, "s2x conv: %dx%d -> %dx%d", a.Hin, a.Win, a.Hout, a.Wout);
   PA_CHECK(a.Hout % TH == 0 && a.Wout % TW == 0, "s2x conv: %dx%d not tiled by %dx%d", a.Hout, a.Wout, TH, TW);
@@ -239,7 +266,8 @@ static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
   const int ntn = a.Cout / BN;
   const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW);
   const int x = xg && nsp % 8 == 0;
-  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT>), dim3(nsp * ntn), dim3(WM * WN * 64), 0, s, a, x);
+  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT, X3>), dim3(nsp * ntn), dim3(WM * WN * 64), 0, s,
+                     a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

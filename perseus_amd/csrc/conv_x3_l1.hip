@@ -1,0 +1,13 @@
+// conv_gx.h X3 (fp16x3 parity mode) instantiation for layer1's 3x3 stride-1 convs
+// (64x64); one file per layer so the fully unrolled kernels compile in parallel.
+#include "conv_gx.h"
+
+namespace pa {
+
+int launch_conv3x3_x3_l1(const ConvArgs& a, hipStream_t s) {
+  if (a.B <= 0) return PA_OK;
+  PA_CHECK(a.Hout == 64 && a.Wout == 64, "x3 conv layer1: %dx%d", a.Hout, a.Wout);
+  return run_gx<16, 16, 1, 64, 4, 2, 64, 3, 1, 0, 1, true, true>(a, true, s);
+}
+
+}  // namespace pa

@@ -1,0 +1,13 @@
+// conv_gx.h X3 (fp16x3 parity mode) instantiation for layer2's 3x3 stride-1 convs
+// (32x32); one file per layer so the fully unrolled kernels compile in parallel.
+#include "conv_gx.h"
+
+namespace pa {
+
+int launch_conv3x3_x3_l2(const ConvArgs& a, hipStream_t s) {
+  if (a.B <= 0) return PA_OK;
+  PA_CHECK(a.Hout == 32 && a.Wout == 32, "x3 conv layer2: %dx%d", a.Hout, a.Wout);
+  return run_gx<16, 16, 1, 64, 4, 2, 128, 3, 1, 0, 1, true, true>(a, true, s);  // BN 64: the residual hi/lo fit in VGPRs
+}
+
+}  // namespace pa

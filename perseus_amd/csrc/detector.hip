@@ -28,8 +28,9 @@ void set_error(const char* fmt, ...) {
 
 struct ConvL {
   int cin, cout, ks, stride, pad;
-  size_t w_off;  // element offset into the packed weight arrays
-  size_t b_off;  // element offset into the bias array
+  size_t w_off;   // element offset into the packed weight arrays (w16 / w32)
+  size_t b_off;   // element offset into the bias / scale arrays
+  size_t w3_off;  // element offset into the fp16x3 weight planes (w3)
 };
 
 struct Block {
@@ -45,6 +46,9 @@ struct pa_detector {
   _Float16* w16 = nullptr;
   float* w32 = nullptr;
   float* bias = nullptr;
+  _Float16* w3 = nullptr;   // fp16x3: per conv [cout][taps][hi (cin) | lo (cin)] of w * 2^e (stem: hi plane, lo plane)
+  float* scl = nullptr;     // fp16x3: 2^-e per output channel (indexed like bias)
+  float* bstem3 = nullptr;  // fp16x3 stem: bias * 2^e (the stem's accumulator starts from it)
   float* fcw = nullptr;
   float* fcb = nullptr;
   char* ws = nullptr;
@@ -69,8 +73,8 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
     pos += n;
     return p;
   };
-  std::vector<_Float16> h16;
-  std::vector<float> h32, hb;
+  std::vector<_Float16> h16, h3;
+  std::vector<float> h32, hb, hs, hbs;
 
   // conv weight + BN -> packed [cout][ks][ks][cin] (stem: [64][7][32])
   auto add_conv = [&](int cin, int cout, int ks, int stride, int pad, bool stem) -> int {
@@ -80,7 +84,7 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
     const float* mu = take(cout);
     const float* var = take(cout);
     if (!w || !g || !b || !mu || !var) return -1;
-    ConvL L{cin, cout, ks, stride, pad, h32.size(), hb.size()};
+    ConvL L{cin, cout, ks, stride, pad, h32.size(), hb.size(), h3.size()};
     const int K = stem ? 7 * 32 : ks * ks * cin;
     std::vector<float> packed((size_t)cout * K, 0.f);
     for (int co = 0; co < cout; ++co) {
@@ -98,9 +102,33 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
       h32.push_back(v);
       h16.push_back((_Float16)v);
     }
+    // fp16x3 planes: the f32 folded weights times 2^e_co (max |w| * 2^e in [2^14, 2^15), so
+    // the lo parts stay normal fp16), split into hi = fp16(v), lo = fp16(v - hi).  The
+    // scaling is exact; the epilogue multiplies by 2^-e_co.
+    const size_t base = h3.size();
+    h3.resize(base + (size_t)cout * K * 2);
+    const int taps = stem ? 7 : ks * ks;
+    const int kt = stem ? 32 : cin;  // elements per tap of one plane
+    for (int co = 0; co < cout; ++co) {
+      float m = 0.f;
+      for (int k = 0; k < K; ++k) m = std::fmax(m, std::fabs(packed[(size_t)co * K + k]));
+      const int e = m > 0.f ? 14 - std::ilogb(m) : 0;
+      hs.push_back(std::ldexp(1.0f, -e));
+      if (stem) hbs.push_back(std::ldexp(hb[L.b_off + co], e));
+      for (int t = 0; t < taps; ++t)
+        for (int c = 0; c < kt; ++c) {
+          const float v = std::ldexp(packed[(size_t)co * K + (size_t)t * kt + c], e);
+          const _Float16 hi = (_Float16)v, lo = (_Float16)(v - (float)hi);
+          if (stem) {  // [plane][64][7][32]
+            h3[base + (size_t)co * K + (size_t)t * kt + c] = hi;
+            h3[base + (size_t)cout * K + (size_t)co * K + (size_t)t * kt + c] = lo;
+          } else {  // [cout][tap][hi (cin) | lo (cin)]
+            h3[base + ((size_t)co * taps + t) * 2 * kt + c] = hi;
+            h3[base + ((size_t)co * taps + t) * 2 * kt + kt + c] = lo;
+          }
+        }
+    }
     d->convs.push_back(L);
-    const double taps = stem ? 7.0 * 7.0 * cin : (double)ks * ks * cin;
-    (void)taps;
     return (int)d->convs.size() - 1;
   };
 
@@ -157,14 +185,23 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
   PA_HIP(hipMemcpy(d->bias, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice));
   PA_HIP(hipMemcpy(d->fcw, fw, (size_t)nout * 512 * sizeof(float), hipMemcpyHostToDevice));
   PA_HIP(hipMemcpy(d->fcb, fb, (size_t)nout * sizeof(float), hipMemcpyHostToDevice));
+  PA_HIP(hipMalloc(&d->w3, h3.size() * sizeof(_Float16)));
+  PA_HIP(hipMalloc(&d->scl, hs.size() * sizeof(float)));
+  PA_HIP(hipMalloc(&d->bstem3, hbs.size() * sizeof(float)));
+  PA_HIP(hipMemcpy(d->w3, h3.data(), h3.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(d->scl, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice));
+  PA_HIP(hipMemcpy(d->bstem3, hbs.data(), hbs.size() * sizeof(float), hipMemcpyHostToDevice));
   return PA_OK;
 }
 
+// Activation workspace: 3 ping-pong maps of B x 64x64x64 (the largest; later layers use
+// a prefix), plus the 128x128 stem map of the unfused fp32 stem.  Element bytes: fp16 2,
+// fp32 4, fp16x3 2 x 2 (hi / lo planes).
+static size_t stem_elems(int B, int prec) { return prec == PA_PREC_FP32 ? (size_t)B * 128 * 128 * 64 : 0; }
 static size_t ws_need(int B, int prec) {
-  const size_t es = prec == PA_PREC_FP32 ? 4 : 2;
-  const size_t stem = (size_t)B * 128 * 128 * 64;
+  const size_t es = prec == PA_PREC_FP16 ? 2 : 4;
   const size_t act = (size_t)B * 64 * 64 * 64;
-  return (stem + 3 * act) * es + 1024;
+  return (stem_elems(B, prec) + 3 * act) * es + 1024;
 }
 
 static int ensure_head(pa_detector* d, int B);
@@ -269,7 +306,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
                      const RgbdSrc* rgbd = nullptr) {
   const T* wts = std::is_same<T, float>::value ? (const T*)d->w32 : (const T*)d->w16;
   T* S = reinterpret_cast<T*>(d->ws);
-  const size_t stem_el = (size_t)B * 128 * 128 * 64;
+  const size_t stem_el = stem_elems(B, d->prec);
   const size_t act_el = (size_t)B * 64 * 64 * 64;
   T* X = S + stem_el;
   T* Tb = X + act_el;
@@ -418,6 +455,98 @@ struct HandleScope {
 // same stream (each chunk already fills the chip many times over).
 constexpr int kChunk = 1024;
 
+// fp16x3 parity mode: every conv as 3 fp16 MFMA products of hi/lo planes,
+// f32 accumulate; same schedule and fusions as the fp16 path (stem + pool fused, stride-2
+// conv + downsample fused, in-place residual), separate head.
+static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof) {
+  _Float16* X = reinterpret_cast<_Float16*>(d->ws);
+  const size_t act_el = (size_t)B * 64 * 64 * 64 * 2;  // two planes
+  _Float16* Tb = X + act_el;
+  _Float16* D = Tb + act_el;
+  if (prof) prof->mark("start");
+  const ConvL& st = d->convs[0];
+  PA_RUN(launch_stem_pool_x3(x, B, d->in_ch, d->w3 + st.w3_off, d->bstem3, d->scl + st.b_off, X, s),
+         "stem_x3_conv7x7_pool");
+  int hw = 64;
+  for (const Block& b : d->blocks) {
+    const ConvL& c1 = d->convs[b.conv1];
+    const ConvL& c2 = d->convs[b.conv2];
+    const int ho = hw / c1.stride;
+    const char* kn = nullptr;
+    const _Float16* res = X;
+    _Float16* out = X;  // identity block: residual add in place (same element, same thread)
+    auto s1 = [&](const ConvArgs& a) -> int {
+      switch (a.Hout) {
+        case 64: kn = "conv3x3x3_l1"; return launch_conv3x3_x3_l1(a, s);
+        case 32: kn = "conv3x3x3_l2"; return launch_conv3x3_x3_l2(a, s);
+        case 16: kn = "conv3x3x3_l3"; return launch_conv3x3_x3_l3(a, s);
+        case 8: kn = "conv3x3x3_l4"; return launch_conv3x3_x3_l4(a, s);
+      }
+      set_error("x3 conv: no configuration for %dx%d", a.Hout, a.Wout);
+      return PA_EINVAL;
+    };
+    ConvArgs a{};
+    a.B = B;
+    a.Hin = hw;
+    a.Win = hw;
+    a.Hout = ho;
+    a.Wout = ho;
+    a.M = B * ho * ho;
+    a.stride = 1;
+    a.pad = 1;
+    if (b.ds >= 0) {
+      const ConvL& cd = d->convs[b.ds];
+      ConvS2Args sa{};
+      sa.in = X;
+      sa.w = d->w3 + c1.w3_off;
+      sa.bias = d->bias + c1.b_off;
+      sa.scale = d->scl + c1.b_off;
+      sa.wds = d->w3 + cd.w3_off;
+      sa.bias2 = d->bias + cd.b_off;
+      sa.scale2 = d->scl + cd.b_off;
+      sa.out = Tb;
+      sa.out2 = D;
+      sa.B = B;
+      sa.Hin = hw;
+      sa.Win = hw;
+      sa.Cin = c1.cin;
+      sa.Hout = ho;
+      sa.Wout = ho;
+      sa.Cout = c1.cout;
+      PA_RUN(launch_conv3x3s2_x3(sa, s, &kn), kn);
+      res = D;
+      out = D;
+    } else {
+      a.in = X;
+      a.w = d->w3 + c1.w3_off;
+      a.bias = d->bias + c1.b_off;
+      a.scale = d->scl + c1.b_off;
+      a.out = Tb;
+      a.Cin = c1.cin;
+      a.Cout = c1.cout;
+      a.epi = EPI_RELU;
+      PA_RUN(s1(a), kn);
+    }
+    ConvArgs b2 = a;
+    b2.Hin = ho;
+    b2.Win = ho;
+    b2.in = Tb;
+    b2.w = d->w3 + c2.w3_off;
+    b2.bias = d->bias + c2.b_off;
+    b2.scale = d->scl + c2.b_off;
+    b2.res = res;
+    b2.out = out;
+    b2.Cin = c2.cin;
+    b2.Cout = c2.cout;
+    b2.epi = EPI_RELU | EPI_RES;
+    PA_RUN(s1(b2), kn);
+    if (b.ds >= 0) std::swap(X, D);
+    hw = ho;
+  }
+  PA_RUN(launch_head_x3(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s), "avgpool_fc_x3");
+  return PA_OK;
+}
+
 static int forward(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof) {
   PA_CHECK(d, "null detector");
   PA_CHECK(B >= 0, "batch %d", B);
@@ -430,8 +559,9 @@ static int forward(pa_detector* d, const float* x, int B, float* y, hipStream_t 
     const int nb = B - off < kChunk ? B - off : kChunk;
     const float* xc = x + off * in_frame;
     float* yc = y + off * out_frame;
-    const int rc = d->prec == PA_PREC_FP32 ? forward_t<float>(d, xc, nb, yc, s, prof)
-                                           : forward_t<_Float16>(d, xc, nb, yc, s, prof);
+    const int rc = d->prec == PA_PREC_FP32     ? forward_t<float>(d, xc, nb, yc, s, prof)
+                   : d->prec == PA_PREC_FP16X3 ? forward_x3(d, xc, nb, yc, s, prof)
+                                               : forward_t<_Float16>(d, xc, nb, yc, s, prof);
     if (rc != PA_OK) return rc;
   }
   return PA_OK;
@@ -512,6 +642,9 @@ void pa_detector_destroy(pa_detector* d) {
   hipFree(d->bias);
   hipFree(d->fcw);
   hipFree(d->fcb);
+  hipFree(d->w3);
+  hipFree(d->scl);
+  hipFree(d->bstem3);
   if (d->ws) hipFree(d->ws);
   if (d->pool) hipFree(d->pool);
   if (d->cnt) hipFree(d->cnt);
@@ -525,7 +658,8 @@ int pa_detector_reserve(pa_detector* d, int max_batch) {
 
 int pa_detector_set_precision(pa_detector* d, int precision) {
   PA_CHECK(d, "null detector");
-  PA_CHECK(precision == PA_PREC_FP16 || precision == PA_PREC_FP32, "precision %d", precision);
+  PA_CHECK(precision == PA_PREC_FP16 || precision == PA_PREC_FP32 || precision == PA_PREC_FP16X3, "precision %d",
+           precision);
   if (precision != d->prec) {
     // keep the same batch capacity for the new element size
     const size_t old = d->ws_bytes;

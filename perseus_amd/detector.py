@@ -244,7 +244,7 @@ class KeypointCNN(nn.Module):
         forward(preprocess_rgbd(rgb, depth, ...))."""
         if rgb.device.type != "cuda" or depth.device.type != "cuda":
             raise RuntimeError("forward_rgbd expects device tensors")
-        if self.precision == "fp32" or self.num_channels != 4:
+        if self.precision != "fp16" or self.num_channels != 4:
             return self.forward(preprocess_rgbd(rgb, depth, self.H, self.W, bgr=bgr, near=near, far=far))
         rgb = rgb.contiguous()
         depth = depth.contiguous().float()

@@ -78,7 +78,7 @@ class StreamingPipeline:
         s = torch.cuda.current_stream(self.dev).cuda_stream
         self.rgb_d.copy_(self.rgb_h, non_blocking=True)
         self.depth_d.copy_(self.depth_h, non_blocking=True)
-        if self.model.precision == "fp32":
+        if self.model.precision != "fp16":  # fp32 / fp16x3: preprocess kernel, then the forward
             _lib.check(L.pa_preprocess_rgbd(self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n, self.sh, self.sw,
                                             int(self.bgr), self.near, self.far, self.H, self.W, self.x.data_ptr(), s),
                        "preprocess")

@@ -68,6 +68,18 @@ def test_rank_shard_3000_frames_forward_and_linearize():
             np.testing.assert_allclose(out[f"j_dyn{q}"][j].cpu().numpy(), H[q], atol=ATOL, rtol=1e-12)
 
 
+def test_fp16x3_batch_over_one_chunk():
+    """The parity mode over a batch larger than the library's 1024-frame chunk: same bits
+    per frame as a small batch, within 1e-3 px of the f64 oracle."""
+    x = torch.from_numpy(synth.synthetic_frames(6, 50)).cuda().repeat(21, 1, 1, 1)  # 1050 frames
+    m = _model("fp16x3")
+    y = m(x)
+    assert torch.equal(m(x[1020:1030]), y[1020:1030])
+    idx = np.array([0, 1023, 1024, 1049])
+    y64 = R.run(synth.synthetic_state_dict(0), x[idx].cpu().numpy(), torch.float64)
+    assert np.abs(y[idx].cpu().numpy() - y64).max() * 127.5 <= 1e-3
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -1,7 +1,8 @@
 """GPU parity of the HIP detector (through the C ABI) against the oracle / golden vectors.
 
 Tolerances (north_star: 1e-3 px on keypoint coordinates; px = 127.5 x normalized):
-  * fp32 parity mode (exact-f32 MFMA, f32 NHWC): max |dpx| <= 1e-3 px vs the reference's
+  * fp32 parity mode (exact-f32 MFMA, f32 NHWC) and fp16x3 (the fast parity mode: hi/lo
+    fp16 planes, 3 fp16 MFMA products per MAC): max |dpx| <= 1e-3 px vs the reference's
     own f32 CPU outputs (golden) and vs the f64 oracle.
   * fp16 mode (the fast path): measured error reported; bound FP16_PX_MAX below.
 """
@@ -40,14 +41,18 @@ def cases():
     return detector_cases()
 
 
+PARITY_MODES = ("fp32", "fp16x3")
+
+
+@pytest.mark.parametrize("precision", PARITY_MODES)
 @pytest.mark.parametrize("idx", range(4))
-def test_fp32_mode_matches_reference_golden(gold, idx):
+def test_parity_modes_match_reference_golden(gold, idx, precision):
     name, seed, x = cases()[idx]
-    m = model(seed, precision="fp32")
+    m = model(seed, precision=precision)
     y = m(torch.from_numpy(x).cuda()).cpu().numpy()
     err_ref = np.abs(y - gold[f"{name}/y_ref_f32"]).max() * PX
     err64 = np.abs(y - gold[f"{name}/y_oracle_f64"]).max() * PX
-    print(f"{name}: fp32 max px err vs ref {err_ref:.3e} vs f64 {err64:.3e}")
+    print(f"{name}: {precision} max px err vs ref {err_ref:.3e} vs f64 {err64:.3e}")
     assert err_ref <= FP32_PX_MAX and err64 <= FP32_PX_MAX
 
 
@@ -63,7 +68,7 @@ def test_fp16_mode_matches_reference_golden(gold, idx):
 
 
 @pytest.mark.parametrize("B", [1, 5, 64])
-@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp16x3", "fp16"])
 def test_batch_sizes_vs_oracle(B, precision):
     x = synth.synthetic_frames(3, B, first=17)
     m = model(0, precision=precision)
@@ -71,7 +76,7 @@ def test_batch_sizes_vs_oracle(B, precision):
     y64 = R.run(synth.synthetic_state_dict(0), x, torch.float64)
     d = np.abs(y - y64).reshape(B, -1, 2) * PX
     l2 = np.sqrt((d ** 2).sum(-1))
-    tol = FP32_PX_MAX if precision == "fp32" else FP16_PX_MAX
+    tol = FP32_PX_MAX if precision in PARITY_MODES else FP16_PX_MAX
     print(f"B={B} {precision}: px-L2 max {l2.max():.3e} mean {l2.mean():.3e}")
     assert l2.max() <= tol
 
@@ -83,14 +88,15 @@ def _int_px(y):
     return px, np.trunc(px).astype(np.int64)
 
 
+@pytest.mark.parametrize("precision", PARITY_MODES)
 @pytest.mark.parametrize("idx", range(4))
-def test_integer_keypoints_fp32_mode_bit_exact(gold, idx):
+def test_integer_keypoints_parity_modes_bit_exact(gold, idx, precision):
     """north_star: bit-exact integer pixel indices.  The GPU keypoints, denormalized by the
     library's postprocess kernel and truncated as streaming.py:143-144 does, equal the
     reference's own integers for every coordinate farther than the 1e-3 px tolerance from
     an integer boundary (closer ones may legitimately round either way)."""
     name, seed, x = cases()[idx]
-    m = model(seed, precision="fp32")
+    m = model(seed, precision=precision)
     y = m(torch.from_numpy(x).cuda())
     px_gpu = denormalize_pixel_coordinates(y).cpu().numpy()
     px_ref, int_ref = _int_px(gold[f"{name}/y_ref_f32"])
@@ -103,7 +109,7 @@ def test_integer_keypoints_fp32_mode_bit_exact(gold, idx):
     assert bad == 0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp16x3", "fp16"])
 def test_integer_keypoints_batch64(precision):
     """Same check on a 64-frame bench batch against the CPU f32 oracle (fp32 mode: zero
     mismatches among safe coordinates; fp16 mode: reported, and bounded by the
@@ -113,7 +119,7 @@ def test_integer_keypoints_batch64(precision):
     y = m(torch.from_numpy(x).cuda()).cpu().numpy()
     px_ref, int_ref = _int_px(R.run(synth.synthetic_state_dict(0), x, torch.float32))
     _, int_gpu = _int_px(y)
-    tol = FP32_PX_MAX if precision == "fp32" else FP16_PX_MAX
+    tol = FP32_PX_MAX if precision in PARITY_MODES else FP16_PX_MAX
     frac = np.abs(px_ref - np.round(px_ref))
     mism = int_gpu != int_ref
     print(f"{precision}: {int(mism.sum())} / {mism.size} integer mismatches "
@@ -121,19 +127,36 @@ def test_integer_keypoints_batch64(precision):
     assert not (mism & (frac > tol)).any()
 
 
-def test_rgb_three_channel_model():
+@pytest.mark.parametrize("precision", PARITY_MODES)
+def test_rgb_three_channel_model(precision):
     x = synth.synthetic_frames(1, 2)[:, :3].copy()
-    m = model(2, in_ch=3, precision="fp32")
+    m = model(2, in_ch=3, precision=precision)
     y = m(torch.from_numpy(x).cuda()).cpu().numpy()
     y64 = R.run(synth.synthetic_state_dict(2, 3), x, torch.float64)
     assert np.abs(y - y64).max() * PX <= FP32_PX_MAX
+
+
+def test_fp16x3_profile_and_precision_switch():
+    """fp16x3 runs its own kernels (stem + pool fused, stride-2 + downsample fused) and a
+    model switched between modes keeps giving each mode's bits."""
+    x = torch.from_numpy(synth.synthetic_frames(0, 8)).cuda()
+    m = model(0, precision="fp16x3")
+    prof, y = m.profile(x)
+    names = [n for n, _ in prof]
+    assert names[0] == "stem_x3_conv7x7_pool" and names[-1] == "avgpool_fc_x3" and len(names) == 18
+    assert names[5] == "conv3x3s2x3_l2" and names[1] == "conv3x3x3_l1"
+    assert torch.equal(y, m(x))
+    m.precision = "fp16"
+    y16 = m(x)
+    m.precision = "fp16x3"
+    assert torch.equal(m(x), y) and not torch.equal(y16, y)
 
 
 def test_batch_invariance_and_determinism():
     """Each frame's keypoints are bit-identical whatever batch it is run in (the
     reduction order over K does not depend on the tile shape) and run to run."""
     x = torch.from_numpy(synth.synthetic_frames(5, 64)).cuda()
-    for prec in ("fp16", "fp32"):
+    for prec in ("fp16", "fp32", "fp16x3"):
         m = model(0, precision=prec)
         y64 = m(x)
         y64b = m(x)
