@@ -2,15 +2,17 @@
 
     python -m perseus_amd.build [--force]
 
-Each csrc/*.hip is compiled to an object in parallel, then linked into
-perseus_amd/lib/libperseus_amd.so (git-ignored, shipped to the GPU box with the
-snapshot).  Rebuilds only when a source or header is newer than the library.
+Each csrc/*.hip is compiled to an object in parallel (perseus_amd/lib/obj/, kept for
+incremental rebuilds: only sources newer than their object, or including a newer
+header, are recompiled), then linked into perseus_amd/lib/libperseus_amd.so
+(git-ignored, shipped to the GPU box with the snapshot).
 """
 
 from __future__ import annotations
 
 import glob
 import os
+import re
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -26,12 +28,42 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mllvm", "-disable-promote-alloca-to-lds
          "-Wno-unused-variable", "-Wno-unused-result"]
 
 
+OBJDIR = os.path.join(LIBDIR, "obj")  # incremental build state (git- and gpurun-ignored)
+
+
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
 def _deps():
     return sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
+
+
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _includes(path, seen=None):
+    """Local headers `path` includes, transitively."""
+    seen = set() if seen is None else seen
+    with open(path) as fh:
+        for name in _INC.findall(fh.read()):
+            h = os.path.normpath(os.path.join(os.path.dirname(path), name))
+            if os.path.exists(h) and h not in seen:
+                seen.add(h)
+                _includes(h, seen)
+    return seen
+
+
+def _obj(src: str) -> str:
+    return os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+
+
+def _stale(src: str) -> bool:
+    o = _obj(src)
+    if not os.path.exists(o):
+        return True
+    t = os.path.getmtime(o)
+    return any(os.path.getmtime(p) > t for p in [src, *_includes(src)])
 
 
 def up_to_date() -> bool:
@@ -42,21 +74,26 @@ def up_to_date() -> bool:
 
 
 def _compile(src: str) -> str:
-    obj = os.path.join(LIBDIR, os.path.basename(src).replace(".hip", ".o"))
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    obj = _obj(src)
+    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    os.replace(obj + ".tmp", obj)
     return obj
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(OBJDIR, exist_ok=True)
     if not force and up_to_date():
         return LIB
     srcs = sources()
-    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
+    todo = [s for s in srcs if force or _stale(s)]
+    # the fully unrolled conv kernels take minutes: start the slowest (largest) first
+    todo.sort(key=lambda p: -os.path.getsize(p) - sum(os.path.getsize(h) for h in _includes(p)))
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(todo)))) as ex:
+        list(ex.map(_compile, todo))
+    objs = [_obj(s) for s in srcs]
     tmp = LIB + ".tmp"
     # -z defs: an unresolved symbol (e.g. a kernel stub the host pass dropped) fails the link
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-z,defs", "-o", tmp, *objs]
@@ -64,10 +101,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB)
-    for o in objs:
-        os.remove(o)
     if verbose:
-        print(f"built {LIB}")
+        print(f"built {LIB} ({len(todo)} of {len(srcs)} objects recompiled)")
     return LIB
 
 

@@ -297,12 +297,18 @@ __device__ __forceinline__ void store_colmajor(double* J, const M6& m, int rows,
     for (int r = 0; r < 6; ++r) J[c * rows + r] = m(r, col0 + c) * (isig ? isig[r] : 1.0);
 }
 
+struct NoMid {
+  __device__ void operator()() const {}
+};
+
 // One PoseDynamicsFactor: inputs point at this factor's records, outputs at its
 // slots (r 6, J0 36, J1 18, J2 18, J3 36 column-major; err 1; any J may be null).
+// `mid` runs after r, J0 and J1 are written and before J2, J3 and err are (traj_kernel:
+// the wave's staging buffer is flushed there and reused for the second half).
+template <typename Mid = NoMid>
 __device__ void dyn_one(const double* __restrict__ T1p, const double* __restrict__ wp, const double* __restrict__ vp,
                         const double* __restrict__ T2p, double dt, int vel_frame, const double* __restrict__ isig,
-                        double* __restrict__ r_out, double* __restrict__ J0, double* __restrict__ J1,
-                        double* __restrict__ J2, double* __restrict__ J3, double* __restrict__ err) {
+                        double* r_out, double* J0, double* J1, double* J2, double* J3, double* err, Mid mid = Mid{}) {
   const Pose T1 = load_pose(T1p);
   const Pose T2 = load_pose(T2p);
   const V3 w = load3(wp);
@@ -321,13 +327,14 @@ __device__ void dyn_one(const double* __restrict__ T1p, const double* __restrict
   for (int k = 0; k < 6; ++k) rs[k] = r[k] * (isig ? isig[k] : 1.0);
 #pragma unroll
   for (int k = 0; k < 6; ++k) r_out[k] = rs[k];
-  if (err) {
-    double e = 0.0;
+  double e = 0.0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) e += rs[k] * rs[k];
-    *err = 0.5 * e;
+  for (int k = 0; k < 6; ++k) e += rs[k] * rs[k];
+  if (!(J0 || J1 || J2 || J3)) {
+    mid();
+    if (err) *err = 0.5 * e;
+    return;
   }
-  if (!(J0 || J1 || J2 || J3)) return;
   // dlog = LogmapDerivative(rel) (:112)
   const M3 Jw = rot_dlog(ew);
   const M3 Qr = compute_q(ew, ev);
@@ -366,8 +373,10 @@ __device__ void dyn_one(const double* __restrict__ T1p, const double* __restrict
   }
   if (J0) store_colmajor(J0, h0, 6, 0, 6, isig);
   if (J1) store_colmajor(J1, dtw, 6, 0, 3, isig);
+  mid();
   if (J2) store_colmajor(J2, h2, 6, 0, 3, isig);
   if (J3) store_colmajor(J3, dlog, 6, 0, 6, isig);  // dlog * I (:130)
+  if (err) *err = 0.5 * e;
 }
 
 __global__ __launch_bounds__(64) void dyn_kernel(int n, const double* __restrict__ T1p, const double* __restrict__ wp,
@@ -495,37 +504,109 @@ __global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restric
 // Config 3: all factors of T trajectories x L frames in one launch, measurements
 // straight from the detector output y (normalized, denormalized here exactly as
 // kornia's denormalize_pixel_coordinates in f32, common.h kornia_denorm).
-// Thread index space: [proj: T*L*K | dyn: T*(L-1) | cv: T*(L-1)].
-__global__ __launch_bounds__(64) void traj_kernel(pa_traj_args a) {
-  const long i = blockIdx.x * 64L + threadIdx.x;
+//
+// One wave (workgroup) per 64 consecutive factors of one kind.  Two launches: the
+// dynamics factors (traj_dyn_kernel: SE(3) exp/log chains, 256 VGPRs, one wave per SIMD)
+// and the projection + constant-velocity factors (traj_proj_kernel: ~80 VGPRs, six waves
+// per SIMD to keep the stores streaming) -- in one kernel every wave got the dynamics
+// code's register allocation.  Outputs are staged per wave in LDS and written as the
+// wave's contiguous slice of each output array, 16 B per lane per store (a lane's own
+// record is 16-288 B of column-major doubles: stored directly, one wave-store instruction
+// would scatter over the whole 1-18 KB slice).
+namespace trj {
+constexpr int STAGE = 64 * 60;  // doubles: dynamics r + J0 + J1 (phase A) / J2 + J3 + err (phase B)
+}
+
+// the wave's n records of `per` doubles, staged at st[lane * per ..], -> dst[0 .. n * per)
+__device__ __forceinline__ void wave_flush(double* __restrict__ dst, const double* st, int n, int per) {
+  const int lane = threadIdx.x & 63, nd = n * per;
+  if (!dst) return;
+  if (((uintptr_t)dst & 15) == 0) {
+    for (int c = lane; c < nd / 2; c += 64)
+      reinterpret_cast<double2*>(dst)[c] = reinterpret_cast<const double2*>(st)[c];
+    if ((nd & 1) && lane == 0) dst[nd - 1] = st[nd - 1];
+  } else {
+    for (int c = lane; c < nd; c += 64) dst[c] = st[c];
+  }
+}
+
+__global__ __launch_bounds__(64) void traj_dyn_kernel(pa_traj_args a) {
+  __shared__ __attribute__((aligned(16))) double st[trj::STAGE];
+  const int lane = threadIdx.x;
+  const long nd = (long)a.T * (a.L - 1);
+  const long w = blockIdx.x;
+  auto sync = [] { lds_barrier(); };  // LDS only: the flushed stores stay in flight
+  {  // PoseDynamicsFactor (l, l+1)
+    const long j0 = w * 64;
+    const int n = (int)(nd - j0 < 64 ? nd - j0 : 64);
+    const long jd = j0 + (lane < n ? lane : n - 1);  // tail lanes recompute the last factor, store nothing
+    const long t = jd / (a.L - 1), f = t * a.L + (jd - t * (a.L - 1));
+    double* sr = st + lane * 6;
+    double* s0 = st + 64 * 6 + lane * 36;
+    double* s1 = st + 64 * 42 + lane * 18;
+    double* s2 = st + lane * 18;
+    double* s3 = st + 64 * 18 + lane * 36;
+    double* se = st + 64 * 54 + lane;
+    const bool J = a.j_dyn0 || a.j_dyn1 || a.j_dyn2 || a.j_dyn3;
+    auto mid = [&] {  // r, J0, J1 staged: write them out, free the buffer
+      sync();
+      wave_flush(a.r_dyn + j0 * 6, st, n, 6);
+      if (a.j_dyn0) wave_flush(a.j_dyn0 + j0 * 36, st + 64 * 6, n, 36);
+      if (a.j_dyn1) wave_flush(a.j_dyn1 + j0 * 18, st + 64 * 42, n, 18);
+      sync();
+    };
+    dyn_one(a.pose + f * 12, a.angvel + f * 3, a.vel + f * 3, a.pose + (f + 1) * 12, a.dt, a.vel_frame, a.isig_dyn,
+            sr, a.j_dyn0 ? s0 : nullptr, a.j_dyn1 ? s1 : nullptr, a.j_dyn2 ? s2 : nullptr, a.j_dyn3 ? s3 : nullptr,
+            a.err_dyn ? se : nullptr, mid);
+    sync();
+    if (J) {
+      if (a.j_dyn2) wave_flush(a.j_dyn2 + j0 * 18, st, n, 18);
+      if (a.j_dyn3) wave_flush(a.j_dyn3 + j0 * 36, st + 64 * 18, n, 36);
+    }
+    if (a.err_dyn) wave_flush(a.err_dyn + j0, st + 64 * 54, n, 1);
+  }
+}
+
+__global__ __launch_bounds__(64) void traj_proj_kernel(pa_traj_args a) {
+  __shared__ __attribute__((aligned(16))) double st[64 * 23];
+  const int lane = threadIdx.x;
   const long F = (long)a.T * a.L;
   const long np = F * a.n_kp, nd = (long)a.T * (a.L - 1);
-  if (i < np) {
+  const long wp = (np + 63) / 64;
+  const long w = blockIdx.x;
+  auto sync = [] { lds_barrier(); };  // LDS only: the flushed stores stay in flight
+  if (w < wp) {  // KeypointProjectionFactor, factor i = f * K + k
+    const long i0 = w * 64;
+    const int n = (int)(np - i0 < 64 ? np - i0 : 64);
+    const long i = i0 + (lane < n ? lane : n - 1);
     const long f = i / a.n_kp;
     const int k = (int)(i - f * a.n_kp);
     const float* yf = a.y + f * 2 * a.n_kp + 2 * k;
     const float px = kornia_denorm(yf[0], a.W);
     const float py = kornia_denorm(yf[1], a.H);
+    int32_t* sst = reinterpret_cast<int32_t*>(st + 64 * 15);
     proj_one(a.pose + f * 12, load3(a.corners + 3 * k), (double)px, (double)py, a.K, a.tcam, a.isig_proj,
-             a.r_proj + i * 2, a.j_proj ? a.j_proj + i * 12 : nullptr, a.err_proj ? a.err_proj + i : nullptr,
-             a.status ? a.status + i : nullptr);
+             st + lane * 2, a.j_proj ? st + 64 * 2 + lane * 12 : nullptr, a.err_proj ? st + 64 * 14 + lane : nullptr,
+             sst + lane);
+    sync();
+    wave_flush(a.r_proj + i0 * 2, st, n, 2);
+    if (a.j_proj) wave_flush(a.j_proj + i0 * 12, st + 64 * 2, n, 12);
+    if (a.err_proj) wave_flush(a.err_proj + i0, st + 64 * 14, n, 1);
+    if (a.status && lane < n) a.status[i0 + lane] = sst[lane];
     return;
   }
-  const long jd = i - np;
-  if (jd < nd) {
-    const long t = jd / (a.L - 1), f = t * a.L + (jd - t * (a.L - 1));
-    dyn_one(a.pose + f * 12, a.angvel + f * 3, a.vel + f * 3, a.pose + (f + 1) * 12, a.dt, a.vel_frame, a.isig_dyn,
-            a.r_dyn + jd * 6, a.j_dyn0 ? a.j_dyn0 + jd * 36 : nullptr, a.j_dyn1 ? a.j_dyn1 + jd * 18 : nullptr,
-            a.j_dyn2 ? a.j_dyn2 + jd * 18 : nullptr, a.j_dyn3 ? a.j_dyn3 + jd * 36 : nullptr,
-            a.err_dyn ? a.err_dyn + jd : nullptr);
-    return;
-  }
-  const long jc = jd - nd;
-  if (jc < nd) {
-    const long t = jc / (a.L - 1), f = t * a.L + (jc - t * (a.L - 1));
-    cv_one(a.vel + f * 3, a.vel + (f + 1) * 3, a.isig_cv, a.r_cv + jc * 3, a.j_cv0 ? a.j_cv0 + jc * 9 : nullptr,
-           a.j_cv1 ? a.j_cv1 + jc * 9 : nullptr, a.err_cv ? a.err_cv + jc : nullptr);
-  }
+  const long c0 = (w - wp) * 64;  // ConstantVelocityFactor (l, l+1)
+  if (c0 >= nd) return;
+  const int n = (int)(nd - c0 < 64 ? nd - c0 : 64);
+  const long jc = c0 + (lane < n ? lane : n - 1);
+  const long t = jc / (a.L - 1), f = t * a.L + (jc - t * (a.L - 1));
+  cv_one(a.vel + f * 3, a.vel + (f + 1) * 3, a.isig_cv, st + lane * 3, a.j_cv0 ? st + 64 * 3 + lane * 9 : nullptr,
+         a.j_cv1 ? st + 64 * 12 + lane * 9 : nullptr, a.err_cv ? st + 64 * 21 + lane : nullptr);
+  sync();
+  wave_flush(a.r_cv + c0 * 3, st, n, 3);
+  if (a.j_cv0) wave_flush(a.j_cv0 + c0 * 9, st + 64 * 3, n, 9);
+  if (a.j_cv1) wave_flush(a.j_cv1 + c0 * 9, st + 64 * 12, n, 9);
+  if (a.err_cv) wave_flush(a.err_cv + c0, st + 64 * 21, n, 1);
 }
 
 }  // namespace pa
@@ -563,8 +644,11 @@ int pa_trajectory_linearize(const pa_traj_args* a, void* stream) {
   PA_CHECK(a->y && a->pose && a->vel && a->angvel && a->corners && a->K, "null input pointer");
   PA_CHECK(a->r_proj && (a->L == 1 || (a->r_dyn && a->r_cv)), "null output pointer");
   PA_CHECK(a->vel_frame == PA_VEL_WORLD || a->vel_frame == PA_VEL_BODY, "vel_frame must be 'world' or 'body'.");
-  const long n = (long)a->T * a->L * a->n_kp + 2L * a->T * (a->L - 1);
-  hipLaunchKernelGGL(pa::traj_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, *a);
+  const long np = (long)a->T * a->L * a->n_kp, nd = (long)a->T * (a->L - 1);
+  if (nd > 0)
+    hipLaunchKernelGGL(pa::traj_dyn_kernel, dim3((unsigned)((nd + 63) / 64)), dim3(64), 0, (hipStream_t)stream, *a);
+  hipLaunchKernelGGL(pa::traj_proj_kernel, dim3((unsigned)((np + 63) / 64 + (nd + 63) / 64)), dim3(64), 0,
+                     (hipStream_t)stream, *a);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
