@@ -337,7 +337,21 @@ def loss_statistics(losses: torch.Tensor) -> dict:
     _lib.check(L.pa_loss_statistics(x.data_ptr(), n, out.data_ptr(), ws.data_ptr(), ws.numel(),
                                     _lib.stream_of(x.device)), "loss_statistics")
     mean, std, mn, mx, med = out.cpu().tolist()
-    return {"mean": mean, "std": std, "min": mn, "max": mx, "median": med}
+    # the reference prints torch f32 reductions (validate.py:165): the f64 results rounded
+    # once to f32 are what an exact f32 reduction returns (torch's own order may differ
+    # from them by a few f32 ulps; tests/test_stats_gpu.py bounds that)
+    f32 = {k: float(np.float32(v)) for k, v in (("mean", mean), ("std", std))}
+    return {"mean": mean, "std": std, "min": mn, "max": mx, "median": med, "mean_f32": f32["mean"],
+            "std_f32": f32["std"]}
+
+
+def validation_report(losses: torch.Tensor) -> str:
+    """The "Validation Loss" block validate.py:162-168 prints, from loss_statistics (device
+    reductions, one 40-byte copy back); values are f32 tensors as torch prints them."""
+    st = loss_statistics(losses)
+    t = lambda v: torch.tensor(v, dtype=torch.float32)  # noqa: E731
+    return "\n".join(["=" * 80, "Validation Loss", f"Mean +/- Stdev: {t(st['mean_f32'])} +/- {t(st['std_f32'])}",
+                      f"Min: {t(st['min'])}", f"Max: {t(st['max'])}", f"Median: {t(st['median'])}", "=" * 80])
 
 
 def preprocess_rgbd(rgb: torch.Tensor, depth: torch.Tensor, H: int = 256, W: int = 256, bgr: bool = True,

@@ -52,6 +52,24 @@ def test_validate_py_pipeline():
     np.testing.assert_allclose(st["mean"], float(ref.double().mean()), rtol=1e-6)
 
 
+@pytest.mark.parametrize("n", [16, 1024, 64 * 16 * 40])
+def test_printed_f32_values_match_torch_f32(n):
+    """validate.py:165 prints torch f32 reductions: the f32 mean / stdev agree with torch's
+    own f32 results to 2 ulps (torch's summation order differs from the device's f64 sums
+    rounded once), and min / max / median bit for bit; the report has validate.py's form."""
+    from perseus_amd.detector import validation_report
+
+    g = torch.Generator().manual_seed(n)
+    x = torch.nn.SmoothL1Loss(beta=1.0, reduction="none")(torch.rand(n, generator=g) * 2 - 1,
+                                                          torch.rand(n, generator=g) * 2 - 1)
+    st = loss_statistics(x.cuda())
+    for key, ref in (("mean_f32", x.mean()), ("std_f32", x.std())):
+        ulp = np.spacing(np.float32(ref.item()))
+        assert abs(st[key] - ref.item()) <= 2 * ulp, (key, st[key], ref.item())
+    rep = validation_report(x.cuda()).splitlines()
+    assert rep[1] == "Validation Loss" and rep[3] == f"Min: {x.min()}" and rep[5] == f"Median: {torch.median(x)}"
+
+
 def test_empty_raises():
     with pytest.raises(RuntimeError):
         loss_statistics(torch.empty(0, device="cuda"))
