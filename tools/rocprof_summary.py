@@ -139,13 +139,40 @@ def main():
                 rp = sum(dur[i] for i in idx) / len(idx)
                 line_ = (f"Agreement: bench roofline kernel `{roof['kernel']}` avg {roof['avg_ms'] * 1e3:.2f} us per "
                          f"launch (HIP events, back-to-back reps)")
-                if stats and syms:
-                    avg = {r["Name"]: float(r["AverageNs"]) / 1e3 for r in csv.DictReader(open(stats))}
-                    if all(syms[i] in avg for i in idx):
-                        st = sum(avg[syms[i]] for i in idx) / len(idx)
-                        line_ += f"; rocprofv3 --stats of the same bench command: {st:.2f} us"
+                btr = find(os.path.join(a.dir, "bench_kt"), "*kernel_trace.csv")
+                if btr and syms:
+                    # the bench command also runs these kernels at B = 1024 (its configs[2] leg), so
+                    # --stats' per-symbol average mixes batch sizes; the median over the same
+                    # command's dispatches is the B = 64 launch (the majority of dispatches)
+                    per = defaultdict(list)
+                    for r in csv.DictReader(open(btr)):
+                        per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                    if all(syms[i] in per for i in idx):
+                        st = sum(statistics.median(per[syms[i]]) for i in idx) / len(idx)
+                        n = sum(len(per[syms[i]]) for i in idx)
+                        line_ += (f"; rocprofv3 --kernel-trace of the same bench command, median over its {n} "
+                                  f"dispatches of the kernel: {st:.2f} us")
                 line_ += f"; kernel trace of plain forwards (cold-er caches): {rp:.2f} us."
                 lines.append(line_)
+    # fp16x3 parity-mode forwards (tools/pmc_forward.py --precision fp16x3 --out DIR/x3)
+    x3n = os.path.join(a.dir, "x3", "names.json")
+    x3t = find(os.path.join(a.dir, "x3_kt"), "*kernel_trace.csv")
+    if os.path.exists(x3n) and x3t:
+        xm = json.load(open(x3n))
+        xn = xm["names"]
+        _, xd = per_launch(forwards(trace_rows(x3t), len(xn)), len(xn))
+        lines += ["## fp16x3 parity mode: per launch (kernel trace of plain forwards, median)", "",
+                  "| # | launch | us |", "|---|---|---|"]
+        lines += [f"| {i:02d} | {nm} | {d:.2f} |" for i, (nm, d) in enumerate(zip(xn, xd))]
+        lines += ["", f"Sum: {sum(xd):.1f} us per forward of {xm['batch']} frames.", ""]
+    fst = find(os.path.join(a.dir, "fac_kt"), "*kernel_stats.csv")
+    if fst:
+        lines += ["## factor path (tools/factor_prof.py: 1000 x 24 linearize + GN step)", "",
+                  "| kernel | calls | avg us |", "|---|---|---|"]
+        for r in csv.DictReader(open(fst)):
+            if ours(r["Name"]) or r["Name"].startswith("pa::") or "pa::" in r["Name"]:
+                lines.append(f"| `{r['Name'][:70]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.2f} |")
+        lines.append("")
     if fb:
         tf = os.path.join(out, "pmc_traffic.json")
         allt = json.load(open(tf)) if os.path.exists(tf) else {}
