@@ -291,7 +291,15 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   const int Cout = a.Cout;
   const int ntn = Cout / BN;
   int tn_idx, sp;
-  if (xg) {
+  if (xg >= 2) {
+    // 2-D XCD split: XCD share x = (spatial group sg, channel group cg), XB = xg channel
+    // groups, so one XCD streams only ntn / XB of the weights (layer4: 1.2 of 4.7 MB, an
+    // L2's worth) and reads 8 / XB of the spatial tiles' inputs
+    const int b = blockIdx.x, x8 = b & 7, i = b >> 3;
+    const int cg = x8 % xg, sg = x8 / xg, ntx = ntn / xg;
+    tn_idx = cg * ntx + i % ntx;
+    sp = sg * (((int)gridDim.x / 8) / ntx) + i / ntx;
+  } else if (xg) {
     // b = 8 i + x (x: XCD share); i = ntn * j + tn  ->  spatial tile 8 j + x
     const int b = blockIdx.x, x8 = b & 7, i = b >> 3;
     tn_idx = i % ntn;
@@ -513,7 +521,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
 
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1,
           bool WT = true, bool X3 = false>
-static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
+static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES) || a.epi == (EPI_RELU | EPI_RES | EPI_HEAD),
            "gx conv: epilogue %d", a.epi);
   PA_CHECK(a.Cin == CIN, "gx conv: Cin %d != %d", a.Cin, CIN);
@@ -522,7 +530,9 @@ static int run_gx(const ConvArgs& a, bool xg, hipStream_t s) {
   const int ntn = a.Cout / BN;
   const int nsp = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW);
   const int tiles = nsp * ntn;
-  const int x = xg && nsp % 8 == 0;  // whole groups of 8 spatial tiles only
+  // whole groups of 8 spatial tiles only; the 2-D split needs XB | ntn and (8 / XB) | nsp
+  const int x = xg >= 2 ? ((8 % xg == 0 && ntn % xg == 0 && nsp % (8 / xg) == 0 && ntn >= xg) ? xg : (nsp % 8 == 0))
+                        : (xg && nsp % 8 == 0);
   PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "gx conv: output over 2 GB");
   PA_CHECK(!X3 || (a.scale && !(a.epi & EPI_HEAD)), "gx conv (fp16x3): scale required, no fused head");
   if (a.epi & EPI_HEAD) {

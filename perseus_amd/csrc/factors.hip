@@ -108,16 +108,26 @@ __device__ __forceinline__ V3 load3(const double* p) { return v3(p[0], p[1], p[2
 
 constexpr double kEps = 2.220446049250313e-16;  // std::numeric_limits<double>::epsilon()
 
-// Rot3::Expmap (so3::ExpmapFunctor)
-__device__ M3 rot_exp(V3 w) {
-  const double th2 = dot(w, w);
-  M3 W = skew(w);
-  if (th2 <= kEps) return add(eye3(), W);
-  const double th = sqrt(th2);
-  double s, c;
-  sincos(th, &s, &c);
-  return add(add(eye3(), W, s / th), mul(W, W), (1.0 - c) / th2);
+// |w| with its sine and cosine, computed once per rotation vector: the exp, its
+// derivative and Barfoot's Q of one vector share them (each called sincos itself)
+struct Ang {
+  double th2, th, s, c;
+};
+__device__ __forceinline__ Ang ang(V3 w) {
+  Ang a;
+  a.th2 = dot(w, w);
+  a.th = sqrt(a.th2);
+  sincos(a.th, &a.s, &a.c);
+  return a;
 }
+
+// Rot3::Expmap (so3::ExpmapFunctor)
+__device__ M3 rot_exp(V3 w, const Ang& a) {
+  M3 W = skew(w);
+  if (a.th2 <= kEps) return add(eye3(), W);
+  return add(add(eye3(), W, a.s / a.th), mul(W, W), (1.0 - a.c) / a.th2);
+}
+__device__ M3 rot_exp(V3 w) { return rot_exp(w, ang(w)); }
 
 // Rot3::Logmap (SO3::Logmap), incl. the trace ~ -1 branch
 __device__ V3 rot_log(const M3& R) {
@@ -166,30 +176,22 @@ __device__ V3 rot_log(const M3& R) {
 }
 
 // SO3 ExpmapDerivative (right Jacobian) and LogmapDerivative (its inverse)
-__device__ M3 rot_dexp(V3 w) {
-  const double th2 = dot(w, w);
+__device__ M3 rot_dexp(V3 w, const Ang& a) {
   M3 W = skew(w);
-  if (th2 <= kEps) return add(eye3(), W, -0.5);
-  const double th = sqrt(th2);
-  double s, c;
-  sincos(th, &s, &c);
-  return add(add(eye3(), W, -(1.0 - c) / th2), mul(W, W), (th - s) / (th2 * th));
+  if (a.th2 <= kEps) return add(eye3(), W, -0.5);
+  return add(add(eye3(), W, -(1.0 - a.c) / a.th2), mul(W, W), (a.th - a.s) / (a.th2 * a.th));
 }
-__device__ M3 rot_dlog(V3 w) {
-  const double th2 = dot(w, w);
-  if (th2 <= kEps) return eye3();
-  const double th = sqrt(th2);
-  double s, c;
-  sincos(th, &s, &c);
+__device__ M3 rot_dlog(V3 w, const Ang& a) {
+  if (a.th2 <= kEps) return eye3();
   M3 W = skew(w);
-  return add(add(eye3(), W, 0.5), mul(W, W), 1.0 / th2 - (1.0 + c) / (2.0 * th * s));
+  return add(add(eye3(), W, 0.5), mul(W, W), 1.0 / a.th2 - (1.0 + a.c) / (2.0 * a.th * a.s));
 }
 
 // Pose3::Expmap
-__device__ Pose pose_exp(V3 w, V3 v) {
+__device__ Pose pose_exp(V3 w, V3 v, const Ang& a) {
   Pose T;
-  T.R = rot_exp(w);
-  const double th2 = dot(w, w);
+  T.R = rot_exp(w, a);
+  const double th2 = a.th2;
   if (th2 > kEps) {
     V3 wxv = cross(w, v);
     T.t = (1.0 / th2) * (wxv - mv(T.R, wxv) + dot(w, v) * w);
@@ -214,20 +216,19 @@ __device__ void pose_log(const Pose& T, V3& w, V3& u) {
 }
 
 // Pose3::ComputeQforExpmapDerivative (Barfoot14tro eq. 102, right Jacobian)
-__device__ M3 compute_q(V3 w, V3 v) {
+__device__ M3 compute_q(V3 w, V3 v, const Ang& a) {
   M3 V = skew(v), W = skew(w);
   M3 WV = mul(W, V), VW = mul(V, W);
   M3 WVW = mul(WV, W);
   M3 WWV = mul(W, WV), VWW = mul(VW, W);
   M3 WVWW = mul(WVW, W), WWVW = mul(W, WVW);
-  const double phi = sqrt(dot(w, w));
+  const double phi = a.th;
   M3 t1 = add(add(WV, VW), WVW, -1.0);
   M3 t2 = add(add(WWV, VWW), WVW, -3.0);
   M3 t3 = add(WVWW, WWVW);
   double c1, c2, c3;
   if (fabs(phi) > 1e-5) {
-    double s, c;
-    sincos(phi, &s, &c);
+    const double s = a.s, c = a.c;
     const double p2 = phi * phi, p3 = p2 * phi, p4 = p2 * p2, p5 = p4 * phi;
     c1 = (phi - s) / p3;
     c2 = (1.0 - p2 / 2.0 - c) / p4;
@@ -274,6 +275,14 @@ __device__ __forceinline__ M6 mul6(const M6& A, const M6& B) {
     }
   return C;
 }
+// block lower-triangular 6x6 [[A, 0], [C, A]]
+struct BL {
+  M3 A, C;
+};
+__device__ __forceinline__ BL mulbl(const BL& X, const BL& Y) {
+  return BL{mul(X.A, Y.A), add(mul(X.C, Y.A), mul(X.A, Y.C))};
+}
+__device__ __forceinline__ BL adjoint_bl(const Pose& T) { return BL{T.R, mul(skew(T.t), T.R)}; }
 // Pose3::AdjointMap = [[R, 0], [skew(t) R, R]]
 __device__ __forceinline__ M6 adjoint(const Pose& T) { return blk(T.R, mul(skew(T.t), T.R)); }
 __device__ __forceinline__ Pose inverse(const Pose& T) {
@@ -316,7 +325,8 @@ __device__ void dyn_one(const double* __restrict__ T1p, const double* __restrict
   V3 vb = v;
   if (vel_frame == PA_VEL_WORLD) vb = mtv(T1.R, v);  // transformTo / unrotate (factors.py:100,134)
   const V3 xw = dt * w, xv = dt * vb;
-  const Pose inc = pose_exp(xw, xv);   // Expmap (:104 / :136)
+  const Ang ax = ang(xw);               // |xi_w| for Expmap, ExpmapDerivative and Q below
+  const Pose inc = pose_exp(xw, xv, ax);  // Expmap (:104 / :136)
   const Pose pred = compose(T1, inc);  // compose (:105)
   const Pose rel = compose(inverse(pred), T2);  // between (:108)
   V3 ew, ev;
@@ -335,47 +345,50 @@ __device__ void dyn_one(const double* __restrict__ T1p, const double* __restrict
     if (err) *err = 0.5 * e;
     return;
   }
+  // Every 6x6 factor below is block lower-triangular [[A, 0], [C, A]] (dexp / dlog /
+  // adjoint form), so each product is three 3x3 products (BL, mulbl).
   // dlog = LogmapDerivative(rel) (:112)
-  const M3 Jw = rot_dlog(ew);
-  const M3 Qr = compute_q(ew, ev);
-  const M6 dlog = blk(Jw, scale(mul(mul(Jw, Qr), Jw), -1.0));
-  // drel_dpred = -Ad(rel^-1); dpred_dx0 = Ad(inc^-1)
-  M6 A = mul6(dlog, adjoint(inverse(rel)));
-#pragma unroll
-  for (int k = 0; k < 36; ++k) A.a[k] = -A.a[k];  // dlog * drel_dpred
-  const M6 H0 = mul6(A, adjoint(inverse(inc)));
+  const Ang ae = ang(ew);
+  const M3 Jw = rot_dlog(ew, ae);
+  const BL dlog{Jw, scale(mul(mul(Jw, compute_q(ew, ev, ae)), Jw), -1.0)};
+  // A = dlog * drel_dpred, drel_dpred = -Ad(rel^-1); H0 = A * Ad(inc^-1)
+  BL A = mulbl(dlog, adjoint_bl(inverse(rel)));
+  A.A = scale(A.A, -1.0);
+  A.C = scale(A.C, -1.0);
+  const BL H0 = mulbl(A, adjoint_bl(inverse(inc)));
   // derr_dtwist = dt * dlog * drel_dpred * I * ExpmapDerivative(xi) (:117)
-  const M3 Jx = rot_dexp(xw);
-  M6 dtw = mul6(A, blk(Jx, compute_q(xw, xv)));
+  BL dtw = mulbl(A, BL{rot_dexp(xw, ax), compute_q(xw, xv, ax)});
+  dtw.A = scale(dtw.A, dt);
+  dtw.C = scale(dtw.C, dt);
+  // J0 = H0 (+ world frame: lower-left += dtw[3:, 3:] skew(vb), :122); its columns 3..5 are [0; H0.A]
+  const M3 C0 = vel_frame == PA_VEL_WORLD ? add(H0.C, mul(dtw.A, skew(vb))) : H0.C;
+  const double s0 = isig ? isig[0] : 1.0, s1 = isig ? isig[1] : 1.0, s2 = isig ? isig[2] : 1.0;
+  const double s3 = isig ? isig[3] : 1.0, s4 = isig ? isig[4] : 1.0, s5 = isig ? isig[5] : 1.0;
+  const double sw[6] = {s0, s1, s2, s3, s4, s5};
+  // column-major 6 x ncols: rows 0..2 from `top`, rows 3..5 from `bot` (null = zero block)
+  auto store = [&](double* J, const M3* top, const M3& bot, int ncols) __attribute__((always_inline)) {
 #pragma unroll
-  for (int k = 0; k < 36; ++k) dtw.a[k] *= dt;
-  M6 h0 = H0;
-  M6 h2;  // columns 0..2 used
-  if (vel_frame == PA_VEL_WORLD) {
-    // H0[:, :3] += dtw[:, 3:] @ skew(vb)  (:122);  H2 = dtw[:, 3:] @ R1^T (:125)
-    const M3 S = skew(vb);
-    for (int r6 = 0; r6 < 6; ++r6)
+    for (int c = 0; c < 3; ++c) {
+      if (c >= ncols) break;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        double s = 0.0, s2 = 0.0;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          s += dtw(r6, 3 + k) * S(k, c);
-          s2 += dtw(r6, 3 + k) * T1.R(c, k);  // (R1^T)(k, c) = R1(c, k)
-        }
-        h0(r6, c) += s;
-        h2(r6, c) = s2;
+      for (int r = 0; r < 3; ++r) {
+        J[c * 6 + r] = (top ? (*top)(r, c) : 0.0) * sw[r];
+        J[c * 6 + 3 + r] = bot(r, c) * sw[3 + r];
       }
-  } else {
-    for (int r6 = 0; r6 < 6; ++r6)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) h2(r6, c) = dtw(r6, 3 + c);  // (:128)
+    }
+  };
+  if (J0) {
+    store(J0, &H0.A, C0, 3);
+    store(J0 + 18, nullptr, H0.A, 3);
   }
-  if (J0) store_colmajor(J0, h0, 6, 0, 6, isig);
-  if (J1) store_colmajor(J1, dtw, 6, 0, 3, isig);
+  if (J1) store(J1, &dtw.A, dtw.C, 3);  // dtw[:, :3] (:117-118)
   mid();
-  if (J2) store_colmajor(J2, h2, 6, 0, 3, isig);
-  if (J3) store_colmajor(J3, dlog, 6, 0, 6, isig);  // dlog * I (:130)
+  // J2 = dtw[:, 3:] @ R1^T (world, :125) or dtw[:, 3:] (body, :128); dtw[:3, 3:] = 0
+  if (J2) store(J2, nullptr, vel_frame == PA_VEL_WORLD ? mul(dtw.A, tr(T1.R)) : dtw.A, 3);
+  if (J3) {  // dlog * I (:130)
+    store(J3, &dlog.A, dlog.C, 3);
+    store(J3 + 18, nullptr, dlog.A, 3);
+  }
   if (err) *err = 0.5 * e;
 }
 
@@ -603,18 +616,21 @@ __device__ __forceinline__ void traj_proj_wave(const pa_traj_args& a, long w, do
 }
 
 // one launch, the dynamics waves dispatched first: they hold the longest per-lane
-// chains (one wave per SIMD at the dynamics code's 256 VGPRs, which every wave of the
-// launch then gets) and the projection / constant-velocity waves fill the other SIMDs
-// meanwhile.  Measured at 1000 x 24: 18.8 us, against 16.1 + 8.9 us as two launches
-// (the projection kernel at 76 VGPRs) and 42 us with the dynamics launch on a forked
-// side stream (the cross-stream event round trips cost more than the overlap won).
-__global__ __launch_bounds__(64) void traj_all_kernel(pa_traj_args a) {
+// chains and the projection / constant-velocity waves fill the other SIMDs meanwhile.
+// Two waves per SIMD (the dynamics code then spills 76 B per lane to scratch: 16.1 us at
+// 1000 x 24, against 17.8 at one wave per SIMD); block-lower-triangular 6x6 products in
+// the dynamics Jacobians (19.0 -> 17.8 us).  Also measured: two launches (the projection
+// kernel at 76 VGPRs) 16.1 + 8.9 us; the dynamics launch on a forked side stream 42 us
+// (the cross-stream event round trips cost more than the overlap won); s_setprio on the
+// dynamics waves: no change.
+__global__ __launch_bounds__(64, 2) void traj_all_kernel(pa_traj_args a) {
   __shared__ __attribute__((aligned(16))) double st[trj::STAGE];
   const long wd = ((long)a.T * (a.L - 1) + 63) / 64;
-  if ((long)blockIdx.x < wd)
+  if ((long)blockIdx.x < wd) {
     traj_dyn_wave(a, blockIdx.x, st);
-  else
+  } else {
     traj_proj_wave(a, blockIdx.x - wd, st);
+  }
 }
 
 }  // namespace pa
