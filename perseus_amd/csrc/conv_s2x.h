@@ -25,7 +25,9 @@
 
 namespace pa {
 
-template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G, bool WT = true, bool X3 = false>
+// DBG = 4: s_memrealtime stamps into a.trace (conv.h trace_stamp: 0 start, 1 prologue landed,
+// 2 K loop done, 3 epilogue stores issued, 63 stores retired)
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G, bool WT = true, bool X3 = false, int DBG = 0>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
@@ -78,6 +80,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     tn_idx = blockIdx.x % ntn;
     sp = blockIdx.x / ntn;
   }
+  if constexpr (DBG == 4) trace_stamp(a.trace, 0);
   const int tw_n = W / TW, tpi = (H / TH) * tw_n;
   const int img = sp / tpi;
   const int rem = sp - img * tpi;
@@ -165,6 +168,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     if (t < NSTEPS) dma_w(t);
   xwait_vm<0>();
   __builtin_amdgcn_s_barrier();
+  if constexpr (DBG == 4) trace_stamp(a.trace, 1);
 
   xu4 fa[2][TN], fb[2][TM];
   auto read_frags = [&](auto kc) __attribute__((always_inline)) {
@@ -221,6 +225,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
       __builtin_amdgcn_s_barrier();
     }
   });
+  if constexpr (DBG == 4) trace_stamp(a.trace, 2);
   xwait_vm<0>();
 
   if (img >= a.B) return;
@@ -253,9 +258,15 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
         store16<WT>(out2, (unsigned)((pixo[tm] + Cout + p * 32) * 2), l2);
       }
     }
+  if constexpr (DBG == 4) {
+    trace_stamp(a.trace, 3);
+    __builtin_amdgcn_s_waitcnt(0);
+    trace_stamp(a.trace, 63);
+  }
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1, bool WT = true, bool X3 = false>
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1, bool WT = true, bool X3 = false,
+          int DBG = 0>
 static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
   PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "s2x conv: output over 2 GB");
   PA_CHECK(!X3 || (a.scale && a.scale2), "s2x conv (fp16x3): scales required");
@@ -266,8 +277,8 @@ static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
   const int ntn = a.Cout / BN;
   const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW);
   const int x = xg && nsp % 8 == 0;
-  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT, X3>), dim3(nsp * ntn), dim3(WM * WN * 64), 0, s,
-                     a, x);
+  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT, X3, DBG>), dim3(nsp * ntn), dim3(WM * WN * 64),
+                     0, s, a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -11,8 +11,7 @@ int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const ch
   if (a.Hout == 32 && a.Cin == 64) {
     if (kname) *kname = "conv3x3s2x_l2";
     if (variant & 8) return run_s2x<8, 16, 128, 4, 2, 64, 3, 1, false>(a, xg, s);  // plain (write-back) stores
-    if (variant == 5) return run_s2x<4, 16, 64, 2, 2, 64, 3>(a, xg, s);  // 72 KB: two workgroups per CU
-    if (variant == 6) return run_s2x<4, 16, 128, 2, 2, 64, 2>(a, xg, s);
+    if (variant == 7 && a.trace) return run_s2x<8, 16, 128, 4, 2, 64, 3, 1, true, false, 4>(a, xg, s);  // timestamps
     switch (variant & 3) {
       case 1: return run_s2x<8, 16, 128, 4, 2, 64, 3, 2>(a, xg, s);
       case 2: return run_s2x<8, 16, 64, 4, 1, 64, 3>(a, xg, s);
@@ -23,7 +22,7 @@ int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const ch
   if (a.Hout == 16 && a.Cin == 128) {
     if (kname) *kname = "conv3x3s2x_l3";
     if (variant & 8) return run_s2x<4, 16, 128, 2, 4, 128, 3, 1, false>(a, xg, s);  // plain (write-back) stores
-    if (variant == 5) return run_s2x<2, 16, 64, 2, 2, 128, 3>(a, xg, s);  // 80 KB: two workgroups per CU
+    if (variant == 7 && a.trace) return run_s2x<4, 16, 128, 2, 4, 128, 3, 1, true, false, 4>(a, xg, s);  // timestamps
     switch (variant & 3) {
       case 1: return run_s2x<4, 16, 128, 2, 4, 128, 3, 2>(a, xg, s);
       case 2: return run_s2x<4, 16, 64, 2, 2, 128, 4>(a, xg, s);
@@ -34,6 +33,7 @@ int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const ch
   if (a.Hout == 8 && a.Cin == 256) {
     if (kname) *kname = "conv3x3s2x_l4";
     if (variant & 8) return run_s2x<8, 8, 128, 2, 4, 256, 3, 1, false>(a, xg, s);  // plain (write-back) stores
+    if (variant == 7 && a.trace) return run_s2x<8, 8, 128, 2, 4, 256, 3, 1, true, false, 4>(a, xg, s);  // timestamps
     switch (variant & 3) {
       case 1: return run_s2x<8, 8, 128, 2, 4, 256, 2>(a, xg, s);
       case 2: return run_s2x<8, 8, 64, 2, 2, 256, 4>(a, xg, s);
