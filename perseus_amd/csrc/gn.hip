@@ -8,10 +8,11 @@
 //   D_l (diagonal): the K projection factors of frame l (pose), the dynamics factors
 //                   (l-1, l) and (l, l+1), the constant-velocity factors around l;
 //   E_l (x_l rows, x_{l+1} cols): the dynamics and constant-velocity factors (l, l+1).
-// Kernel 1 (gn_assemble): one wave per frame builds D_l, E_l, g_l = J^T r from the
-// factors touching it -- each block has one writer, no atomics.  Kernel 2 (gn_solve):
-// one wave per trajectory, block Cholesky (L_l L_l^T = D_l + lambda I - W_l^T W_l,
-// W_l = L_{l-1}^{-1} E_{l-1}), forward and back substitution.  f64 throughout.
+// One launch (gn_step_kernel), one two-wave workgroup per trajectory: wave 0 assembles
+// D_l, E_l, g_l = J^T r of frame l + 1 from the factors touching it (each block has one
+// writer, no atomics) into an LDS ring while wave 1 factors frame l -- block Cholesky
+// (L_l L_l^T = D_l + lambda I - W_l^T W_l, W_l = L_{l-1}^{-1} E_{l-1}), forward and back
+// substitution.  D / E / g are also written out (the API's outputs).  f64 throughout.
 // Jacobians are column-major per factor (include/perseus_amd.h).
 #include "common.h"
 
@@ -34,7 +35,7 @@ struct GnArgs {
 };
 
 // ---------------------------------------------------------------- assembly
-// One wave per frame l (of trajectory t).  The factor rows touching x_l are stacked in
+// One wave, frame l (of trajectory t).  The factor rows touching x_l are stacked in
 // LDS, transposed, as A^T (12 x R, in x_l coordinates; zero rows for cheirality-failed
 // projections) with their residuals r, and the rows of the factors (l, l+1) also as the
 // 12 x 10 pair (A_next^T, B^T) (B: their x_{l+1} part):
@@ -47,15 +48,28 @@ struct GnArgs {
 // columns, or one g entry) over the wave's lanes, reading 2 rows per 16-B LDS read.
 constexpr int GN_KMAX = 16;  // keypoints per frame supported
 constexpr int GN_WSF = 2 * gn::NB + 2 * gn::NV;  // workspace doubles per frame: L_l, W_l, y_l, 1 / diag(L_l)
-template <int RP>  // stacked rows, padded to even: 2 K + 18 (+1)
-__global__ __launch_bounds__(64, 8) void gn_assemble(GnArgs a) {
+// wave-local LDS ordering (one wave's ds ops run in order; the wait and the "memory" clobber
+// keep the compiler from moving LDS accesses across it)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int RP>
+struct GnStage {
+  double AT[gn::NV][RP];
+  double rT[RP];
+  double ANT[gn::NV][10];
+  double BT[gn::NV][10];
+};
+
+// Assembles frame f (of trajectory t, frame index l) with one wave: D_l, E_l (if l + 1 < L)
+// and g_l to the outputs a.D / a.E / a.g and to the LDS block `blk` (D | E | g).
+template <int RP>
+__device__ __forceinline__ void gn_assemble_frame(const GnArgs& a, long f, GnStage<RP>& st, double* blk) {
   using namespace gn;
-  __shared__ __attribute__((aligned(16))) double AT[NV][RP];
-  __shared__ __attribute__((aligned(16))) double rT[RP];
-  __shared__ __attribute__((aligned(16))) double ANT[NV][10];
-  __shared__ __attribute__((aligned(16))) double BT[NV][10];
-  const int lane = threadIdx.x;
-  const long f = blockIdx.x;
+  double(&AT)[NV][RP] = st.AT;
+  double(&rT)[RP] = st.rT;
+  double(&ANT)[NV][10] = st.ANT;
+  double(&BT)[NV][10] = st.BT;
+  const int lane = threadIdx.x & 63;
   const int t = (int)(f / a.L), l = (int)(f - (long)t * a.L);
   const int npair = a.L - 1;
   const int K = a.K;
@@ -66,7 +80,7 @@ __global__ __launch_bounds__(64, 8) void gn_assemble(GnArgs a) {
     (&BT[0][0])[e] = 0.0;
   }
   for (int e = lane; e < RP; e += 64) rT[e] = 0.0;
-  __syncthreads();
+  wave_lds_sync();
   // projections: rows 2k, 2k + 1; J column-major 2 x 6
   for (int e = lane; e < K * 12; e += 64) {
     const int k = e / 12, c = (e - k * 12) >> 1, row = e & 1;
@@ -119,7 +133,7 @@ __global__ __launch_bounds__(64, 8) void gn_assemble(GnArgs a) {
       rT[rp + 6 + lane - 51] = a.r_cv[u * 3 + lane - 51];
     }
   }
-  __syncthreads();
+  wave_lds_sync();
   typedef double d2_t __attribute__((ext_vector_type(2)));
   double* Dl = a.D + f * NB;
   double* El = nxt ? a.E + ((long)t * npair + l) * NB : nullptr;
@@ -143,7 +157,11 @@ __global__ __launch_bounds__(64, 8) void gn_assemble(GnArgs a) {
           }
         }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) Dl[i * NV + j0 + c] = s[c][0] + s[c][1];
+        for (int c = 0; c < 3; ++c) {
+          const double v = s[c][0] + s[c][1];
+          Dl[i * NV + j0 + c] = v;
+          blk[i * NV + j0 + c] = v;
+        }
       } else {
 #pragma unroll
         for (int q = 0; q < 10; q += 2) {
@@ -156,7 +174,11 @@ __global__ __launch_bounds__(64, 8) void gn_assemble(GnArgs a) {
           }
         }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) El[i * NV + j0 + c] = s[c][0] + s[c][1];
+        for (int c = 0; c < 3; ++c) {
+          const double v = s[c][0] + s[c][1];
+          El[i * NV + j0 + c] = v;
+          blk[NB + i * NV + j0 + c] = v;
+        }
       }
     } else {  // g[i]
       const int i = w - 96;
@@ -169,12 +191,13 @@ __global__ __launch_bounds__(64, 8) void gn_assemble(GnArgs a) {
         s1 += ai[1] * r[1];
       }
       gl[i] = s0 + s1;
+      blk[2 * NB + i] = s0 + s1;
     }
   }
 }
 
 // ---------------------------------------------------------------- solve
-// One wave per trajectory: block Cholesky of the block-tridiagonal normal matrix, frame
+// The solver wave of a trajectory: block Cholesky of the block-tridiagonal normal matrix, frame
 // by frame,
 //   W_l = L_{l-1}^{-1} E_{l-1}                 lane c < 12: column c, forward substitution
 //                                              with L_{l-1} read from LDS (uniform addresses)
@@ -184,8 +207,11 @@ __global__ __launch_bounds__(64, 8) void gn_assemble(GnArgs a) {
 //                                              raw column j reaches every lane by v_readlane
 //   y_l = L_l^{-1} rhs_l
 // then back substitution L_l^T delta_l = y_l - W_{l+1} delta_{l+1}.  L_l, W_l, y_l go to the
-// workspace for the backward pass.  The next frame's D / E / g rows are loaded while the
-// current frame is factored.  (Round 1 ran one thread per trajectory with the blocks in
+// workspace for the backward pass.  Frame l's D / E / g come from the LDS ring, built by
+// the assembler wave during frame l - 1 (one LDS-only barrier per frame hands a slot
+// over; the solver's own LDS exchanges are wave-local).  Round 2a ran assembly (one
+// wave per frame) and solve (one wave per trajectory) as two launches: 54 + 175 us per
+// 1000 x 24.  (Round 1 ran one thread per trajectory with the blocks in
 // LDS, 16-thread workgroups: 2.2 ms per 1000 x 24.)
 // 1 / sqrt(x) for x > 0: the hardware estimate + two Newton steps (f64 accurate; the IEEE
 // sqrt + divide sequences were a third of the solve's instructions)
@@ -204,134 +230,160 @@ __device__ __forceinline__ double gn_bcast(double v, int src) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-__global__ __launch_bounds__(64) void gn_solve(GnArgs a) {
+__device__ __forceinline__ int lds_load_acquire(const int* p) {
+  const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  return v;
+}
+__device__ __forceinline__ void lds_store_release(int* p, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS only: global stores stay in flight
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// NA assembler waves (wave a builds frames a, a + NA, ...) and one solver wave per
+// trajectory, handing frames over through an LDS ring of NA + 2 slots with two LDS
+// counters: ready[slot] = frame + 1 once the slot holds that frame, `consumed` = frames
+// the solver has finished (frame m may overwrite slot m % R once the solver is past frame
+// m - R + 1, whose E block it reads last).  Every wait is satisfied by waves of the same
+// workgroup that are already running, and the solver publishes `consumed` even for frames
+// it skips after a failed pivot, so every wave runs to its end.
+template <int RP, int NA>
+__global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
   using namespace gn;
-  __shared__ __attribute__((aligned(16))) double Lp[NB];  // L_{l-1}, row-major
-  __shared__ double Ld[NV];                                 // 1 / L_{l-1}[i][i]
-  __shared__ __attribute__((aligned(16))) double Wt[NB];  // W_l^T: row c = column c of W
-  __shared__ __attribute__((aligned(16))) double ys[NV];  // y_{l-1}
-  const int t = blockIdx.x, i = threadIdx.x;
+  constexpr int BLK = 2 * NB + NV;  // D | E | g of one frame
+  constexpr int R = NA + 2;
+  __shared__ __attribute__((aligned(16))) GnStage<RP> st[NA];  // assembler staging
+  __shared__ __attribute__((aligned(16))) double blk[R][BLK];   // frame ring
+  __shared__ __attribute__((aligned(16))) double Lp[NB];        // L_{l-1}, row-major
+  __shared__ double Ld[NV];                                     // 1 / L_{l-1}[i][i]
+  __shared__ __attribute__((aligned(16))) double Wt[NB];        // W_l^T: row c = column c of W
+  __shared__ __attribute__((aligned(16))) double ys[NV];        // y_{l-1}
+  __shared__ int ready[R];
+  __shared__ int consumed;
+  const int t = blockIdx.x;
+  const int wv = threadIdx.x >> 6;
+  const int i = threadIdx.x & 63;
+  const int L = a.L;
+  const long f0 = (long)t * L;
+  if (threadIdx.x < R) ready[threadIdx.x] = 0;
+  if (threadIdx.x == 0) consumed = 0;
+  __syncthreads();
+  if (wv < NA) {
+    for (int l = wv; l < L; l += NA) {
+      while (lds_load_acquire(&consumed) < l - R + 2) __builtin_amdgcn_s_sleep(2);
+      gn_assemble_frame<RP>(a, f0 + l, st[wv], blk[l % R]);
+      if (i == 0) lds_store_release(&ready[l % R], l + 1);
+    }
+    return;
+  }
   const int ic = i < NV ? i : NV - 1;  // lanes >= 12 shadow row / column 11 (no stores)
   const bool act = i < NV;
-  const int L = a.L, npair = L - 1;
   double* ws = a.ws + (size_t)t * L * GN_WSF;
-  // frame-l operands, loaded one frame ahead: row ic of D_l, column ic of E_{l-1}, g_l[ic]
-  double Dn[NV], En[NV], gn_;
-  auto load = [&](int l) {
-    const size_t f = (size_t)t * L + l;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) Dn[j] = a.D[f * NB + ic * NV + j];
-    gn_ = a.g[f * NV + ic];
-    if (l > 0) {
-      const double* Ep = a.E + ((size_t)t * npair + l - 1) * NB;
-#pragma unroll
-      for (int k = 0; k < NV; ++k) En[k] = Ep[k * NV + ic];
-    }
-  };
-  load(0);
   int info = 0;
   for (int l = 0; l < L; ++l) {
-    double* wl = ws + (size_t)l * GN_WSF;
-    double S[NV], Ec[NV];
+    const int cur = l % R, prv = (l + R - 1) % R;
+    while (lds_load_acquire(&ready[cur]) != l + 1) __builtin_amdgcn_s_sleep(1);
+    if (!info) {
+      double* wl = ws + (size_t)l * GN_WSF;
+      const double* bc = blk[cur];
+      const double* bp = blk[prv];
+      double S[NV];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      S[j] = Dn[j] + (j == ic ? a.lambda : 0.0);
-      Ec[j] = En[j];
-    }
-    double rhs = -gn_;
-    if (l + 1 < L) load(l + 1);
-    if (l > 0) {
-      // W column ic: L_{l-1} w = E_{l-1}[:, ic]
-      double w[NV];
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        double s0 = Ec[k], s1 = 0.0;
-#pragma unroll
-        for (int m = 0; m < k; ++m) {
-          if (m & 1)
-            s1 -= Lp[k * NV + m] * w[m];
-          else
-            s0 -= Lp[k * NV + m] * w[m];
-        }
-        w[k] = (s0 + s1) * Ld[k];
-      }
-      if (act) {
+      for (int j = 0; j < NV; ++j) S[j] = bc[ic * NV + j] + (j == ic ? a.lambda : 0.0);
+      double rhs = -bc[2 * NB + ic];
+      if (l > 0) {
+        // W column ic: L_{l-1} w = E_{l-1}[:, ic]
+        double w[NV];
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
-          Wt[i * NV + k] = w[k];
-          wl[NB + k * NV + i] = w[k];  // W_l row-major in the workspace
-        }
-      }
-      lds_barrier();  // LDS only (a full barrier would drain the stores and the prefetch)
-      // S[ic][j] -= sum_k W[k][ic] W[k][j];  rhs -= sum_k W[k][ic] y_{l-1}[k]
+          double s0 = bp[NB + k * NV + ic], s1 = 0.0;
 #pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        double s0 = 0.0, s1 = 0.0;
+          for (int m = 0; m < k; ++m) {
+            if (m & 1)
+              s1 -= Lp[k * NV + m] * w[m];
+            else
+              s0 -= Lp[k * NV + m] * w[m];
+          }
+          w[k] = (s0 + s1) * Ld[k];
+        }
+        if (act) {
+#pragma unroll
+          for (int k = 0; k < NV; ++k) {
+            Wt[i * NV + k] = w[k];
+            wl[NB + k * NV + i] = w[k];  // W_l row-major in the workspace
+          }
+        }
+        wave_lds_sync();
+        // S[ic][j] -= sum_k W[k][ic] W[k][j];  rhs -= sum_k W[k][ic] y_{l-1}[k]
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < NV; k += 2) {
+            s0 += w[k] * Wt[j * NV + k];
+            s1 += w[k + 1] * Wt[j * NV + k + 1];
+          }
+          S[j] -= s0 + s1;
+        }
+        double r0 = 0.0, r1 = 0.0;
 #pragma unroll
         for (int k = 0; k < NV; k += 2) {
-          s0 += w[k] * Wt[j * NV + k];
-          s1 += w[k + 1] * Wt[j * NV + k + 1];
+          r0 += w[k] * ys[k];
+          r1 += w[k + 1] * ys[k + 1];
         }
-        S[j] -= s0 + s1;
+        rhs -= r0 + r1;
       }
-      double r0 = 0.0, r1 = 0.0;
-#pragma unroll
-      for (int k = 0; k < NV; k += 2) {
-        r0 += w[k] * ys[k];
-        r1 += w[k + 1] * ys[k + 1];
-      }
-      rhs -= r0 + r1;
-    }
-    // S = L L^T, right-looking; lane ic's S becomes row ic of L (a non-positive pivot sets
-    // `bad`; the loop runs on with a dummy pivot so it stays fully unrolled)
-    bool bad = false;
-    double invd = 1.0;  // 1 / L[ic][ic]
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      double col[NV];  // raw column j: S[m][j], final for m >= j
-#pragma unroll
-      for (int m = j; m < NV; ++m) col[m] = gn_bcast(S[j], m);
-      double d2 = col[j];
-      if (!(d2 > 0.0)) {
-        bad = true;
-        d2 = 1.0;
-      }
-      const double inv = gn_rsqrt(d2);
-      const double lij = S[j] * inv;  // L[ic][j] for ic > j
-      if (ic >= j) S[j] = ic == j ? d2 * inv : lij;
-      invd = ic == j ? inv : invd;
-#pragma unroll
-      for (int m = j + 1; m < NV; ++m)
-        if (ic > j) S[m] -= lij * (col[m] * inv);
-    }
-    if (bad) {
-      info = l + 1;
-      break;
-    }
-#pragma unroll
-    for (int j = 0; j < NV; ++j)
-      if (j > ic) S[j] = 0.0;
-    // y = L^{-1} rhs
-    double y[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      if (ic == k) rhs *= invd;
-      y[k] = gn_bcast(rhs, k);
-      if (ic > k) rhs -= S[k] * y[k];
-    }
-    lds_barrier();  // every lane is past its reads of Lp / Ld / Wt / ys
-    if (act) {
+      // S = L L^T, right-looking; lane ic's S becomes row ic of L (a non-positive pivot sets
+      // `bad`; the loop runs on with a dummy pivot so it stays fully unrolled)
+      bool bad = false;
+      double invd = 1.0;  // 1 / L[ic][ic]
 #pragma unroll
       for (int j = 0; j < NV; ++j) {
-        Lp[i * NV + j] = S[j];
-        wl[i * NV + j] = S[j];
+        double col[NV];  // raw column j: S[m][j], final for m >= j
+#pragma unroll
+        for (int m = j; m < NV; ++m) col[m] = gn_bcast(S[j], m);
+        double d2 = col[j];
+        if (!(d2 > 0.0)) {
+          bad = true;
+          d2 = 1.0;
+        }
+        const double inv = gn_rsqrt(d2);
+        const double lij = S[j] * inv;  // L[ic][j] for ic > j
+        if (ic >= j) S[j] = ic == j ? d2 * inv : lij;
+        invd = ic == j ? inv : invd;
+#pragma unroll
+        for (int m = j + 1; m < NV; ++m)
+          if (ic > j) S[m] -= lij * (col[m] * inv);
       }
-      Ld[i] = invd;
-      ys[i] = y[i];
-      wl[2 * NB + i] = y[i];
-      wl[2 * NB + NV + i] = invd;
+      if (bad) {
+        info = l + 1;  // the solver wave idles through the remaining frames' barriers
+      } else {
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+          if (j > ic) S[j] = 0.0;
+        // y = L^{-1} rhs
+        double y[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          if (ic == k) rhs *= invd;
+          y[k] = gn_bcast(rhs, k);
+          if (ic > k) rhs -= S[k] * y[k];
+        }
+        wave_lds_sync();  // every lane is past its reads of Lp / Ld / Wt / ys
+        if (act) {
+#pragma unroll
+          for (int j = 0; j < NV; ++j) {
+            Lp[i * NV + j] = S[j];
+            wl[i * NV + j] = S[j];
+          }
+          Ld[i] = invd;
+          ys[i] = y[i];
+          wl[2 * NB + i] = y[i];
+          wl[2 * NB + NV + i] = invd;
+        }
+      }
     }
-    lds_barrier();
+    if (i == 0) lds_store_release(&consumed, l + 1);
   }
   if (!info) {
     double xn[NV];
@@ -411,12 +463,11 @@ int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const do
   const pa::GnArgs a{T,     L,      n_kp,   r_proj, j_proj, status_proj, r_dyn, j_dyn0, j_dyn1, j_dyn2, j_dyn3,
                      r_cv,  j_cv0,  j_cv1,  lambda, D,      E,           g,     delta,  info,   (double*)ws};
   const hipStream_t s = (hipStream_t)stream;
-  const int F = T * L;
+  constexpr int GN_NA = 2;  // assembler waves per trajectory
   if (n_kp == 8)
-    hipLaunchKernelGGL(pa::gn_assemble<34>, dim3(F), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((pa::gn_step_kernel<34, GN_NA>), dim3(T), dim3(64 * (GN_NA + 1)), 0, s, a);
   else
-    hipLaunchKernelGGL(pa::gn_assemble<2 * pa::GN_KMAX + 18>, dim3(F), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(pa::gn_solve, dim3(T), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((pa::gn_step_kernel<2 * pa::GN_KMAX + 18, GN_NA>), dim3(T), dim3(64 * (GN_NA + 1)), 0, s, a);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -187,6 +187,29 @@ def test_empty_batch_and_reload():
     assert not torch.equal(y0, y7)
 
 
+def test_refresh_weights_after_data_write():
+    """Writes through .data bypass the version counters the weight fingerprint reads;
+    refresh_weights() re-uploads."""
+    m = model(0)
+    x = torch.from_numpy(synth.synthetic_frames(0, 2)).cuda()
+    y0 = m(x)
+    m.resnet.fc.bias.data[0] += 1.0
+    m.refresh_weights()
+    y1 = m(x)
+    assert not torch.equal(y0[:, 0], y1[:, 0]) and torch.equal(y0[:, 1:], y1[:, 1:])
+
+
+def test_batch_over_4096_frames_in_chunks():
+    """B > 4096 (32-bit activation offsets): the library runs 1024-frame chunks; each frame
+    gets the bits it gets in a small batch."""
+    x = torch.from_numpy(synth.synthetic_frames(8, 41)).cuda().repeat(100, 1, 1, 1)  # 4100 frames
+    m = model(0)
+    y = m(x)
+    assert y.shape == (4100, 16)
+    for i in (0, 1023, 1024, 4095, 4099):
+        assert torch.equal(m(x[i:i + 1])[0], y[i]), i
+
+
 def test_postprocess_matches_validate_py():
     y = torch.rand(4, 16, device="cuda") * 2 - 1
     t = torch.rand(4, 16, device="cuda") * 2 - 1

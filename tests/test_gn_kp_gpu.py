@@ -1,0 +1,50 @@
+"""pa_trajectory_gn_step with keypoint counts other than 8 (the kernel's general stacked-row
+instantiation, RP = 2 * GN_KMAX + 18) against the dense f64 oracle (oracle/gn_ref.py), and
+trajectory counts that leave most of the chip idle or oversubscribe it.  Same tolerances
+as test_gn_gpu.py."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gn_ref as G
+from perseus_amd import pipeline
+
+from test_pipeline_gpu import CORNERS, KCAL, _problem  # tests/ is on sys.path (rootdir conftest)
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-9
+S = 0.0175
+FACES = np.array([[S, 0, 0], [-S, 0, 0], [0, S, 0], [0, -S, 0], [0, 0, S], [0, 0, -S]])
+
+
+def _check(corners, T, L, lam, seed):
+    K = len(corners)
+    poses, vels, angvels, _ = _problem(T, L, seed)
+    y = np.random.default_rng(seed + 1).uniform(-1, 1, (T * L, 2 * K)).astype(np.float32)
+    lin = pipeline.linearize_trajectories(torch.as_tensor(y, device="cuda"), poses, vels, angvels, corners, KCAL,
+                                          T=T, L=L, dt=0.1, proj_sigmas=np.array([2.0, 2.0]),
+                                          dyn_sigmas=np.full(6, 0.05), cv_sigmas=np.full(3, 0.5))
+    out = pipeline.gn_step(lin, T=T, L=L, lam=lam)
+    keys = ("r_proj", "j_proj", "status", "r_dyn", "j_dyn0", "j_dyn1", "j_dyn2", "j_dyn3", "r_cv", "j_cv0", "j_cv1")
+    H, g, d = G.gn_step({k: lin[k].cpu().numpy() for k in keys}, T, L, K, lam)
+    assert (out["info"].cpu().numpy() == 0).all()
+    Dd, Ed = out["D"].cpu().numpy(), out["E"].cpu().numpy()
+    for t in range(T):
+        D, E = G.blocks(H[t], L)
+        scale = np.abs(H[t]).max()
+        np.testing.assert_allclose(Dd[t * L:(t + 1) * L], D, rtol=RTOL, atol=RTOL * scale)
+        if L > 1:
+            np.testing.assert_allclose(Ed[t * (L - 1):(t + 1) * (L - 1)], E, rtol=RTOL, atol=RTOL * scale)
+    np.testing.assert_allclose(out["g"].cpu().numpy().reshape(T, -1), g, rtol=RTOL, atol=RTOL * np.abs(g).max())
+    np.testing.assert_allclose(out["delta"].cpu().numpy().reshape(T, -1), d, rtol=1e-7, atol=1e-9 * np.abs(d).max())
+
+
+@pytest.mark.parametrize("corners", [CORNERS[:4], np.concatenate([CORNERS, FACES]), CORNERS[:1]],
+                         ids=["K4", "K14", "K1"])
+def test_gn_step_other_keypoint_counts(corners):
+    _check(corners, 3, 7, 1e-3, 21)
+
+
+def test_gn_step_many_trajectories():
+    """600 trajectories: several workgroups per CU, slot reuse over 13 frames."""
+    _check(CORNERS, 600, 13, 1e-2, 4)

@@ -58,3 +58,19 @@ def test_matches_reference_frame_arithmetic(model):
     assert torch.equal(x, x_dev)
     y = model(x).reshape(3, -1, 2)
     np.testing.assert_array_equal(out, R.denormalize_f32(y.cpu().numpy().reshape(3, -1)))
+
+
+def test_graph_survives_model_reallocation_and_reload():
+    """The captured graph holds its own handle: a later larger-batch forward
+    (which grows the model's workspace) and a weight reload (which destroys the model's
+    handle) must not touch the memory the graph replays into."""
+    m = KeypointCNN(num_channels=4)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
+    rgb, d = _frames(4)
+    g = StreamingPipeline(m, graph=True)
+    ref = g(rgb, d)
+    m(torch.from_numpy(synth.synthetic_frames(0, 64)).cuda())  # B=64: the model's own workspace grows
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(9).items()})
+    m(torch.from_numpy(synth.synthetic_frames(0, 2)).cuda())  # new weights: the model's handle is recreated
+    np.testing.assert_array_equal(g(rgb, d), ref)  # the pipeline keeps the weights it was built with
+    g.close()
