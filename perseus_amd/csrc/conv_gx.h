@@ -91,15 +91,18 @@ __device__ __forceinline__ void xdma16(const void* src, char* lds) {
 // Issue schedule (per wave), used at compile time.
 struct GxPlan {
   int nsteps, ncb, pd, wdma, pdma, rl, rs, g;
-  int spb = 9;  // steps per 64-channel block (9 taps; conv_s2x.h adds the downsample)
+  int spb = 9;     // steps per 64-channel block (9 taps; conv_s2x.h adds the downsample)
+  int spt = 0;     // multi-tile workgroups (conv_s2x.h TPW > 1): steps per tile; the
+  int nstore = 0;  // previous tile's `nstore` output stores open every tile's first step
   // the patch of block c >= 1 is DMA'd at the first group start inside block c - 1
   constexpr int ps(int c) const { return (spb * (c - 1) + g - 1) / g * g; }
+  constexpr int ns(int t) const { return (spt && t > 0 && t % spt == 0) ? nstore : 0; }
   constexpr int nw(int t) const { return t + pd < nsteps ? wdma : 0; }
   constexpr int np(int t) const { return (t / spb + 1 < ncb && t == ps(t / spb + 1)) ? pdma : 0; }
   constexpr int nr(int t) const { return t == rs ? rl : 0; }
   constexpr int cum(int t) const {  // VMEM ops issued in steps 0..t (prologue excluded: it is drained)
     int c = 0;
-    for (int u = 0; u <= t; ++u) c += nw(u) + np(u) + nr(u);
+    for (int u = 0; u <= t; ++u) c += ns(u) + nw(u) + np(u) + nr(u);
     return c;
   }
   // ops issued after the newest op that the fragments of step v need
@@ -108,13 +111,13 @@ struct GxPlan {
     int need = 0;  // issue position just past the newest needed op (0 = all in the prologue)
     if (v >= pd) {
       const int t = v - pd;
-      const int e = (t > 0 ? cum(t - 1) : 0) + nw(t);
+      const int e = (t > 0 ? cum(t - 1) : 0) + ns(t) + nw(t);
       need = e > need ? e : need;
     }
     const int cb = v / spb;
     if (cb >= 1) {
       const int t = ps(cb);
-      const int e = (t > 0 ? cum(t - 1) : 0) + nw(t) + np(t);
+      const int e = (t > 0 ? cum(t - 1) : 0) + ns(t) + nw(t) + np(t);
       need = e > need ? e : need;
     }
     const int n = cum(s) - need;

@@ -312,9 +312,9 @@ template <typename T>
 int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
   if constexpr (std::is_same<T, _Float16>::value) {
-    // conv_s2x (shipped; g_variant[6] = 10..19 its alternatives); 3: the one-tile
+    // conv_s2x (shipped; g_variant[6] = 10..39 its alternatives 0..29); 3: the one-tile
     // kernel below (bit-identical reference for the variant test)
-    if (g_variant[6] == 0 || (g_variant[6] >= 10 && g_variant[6] <= 19))
+    if (g_variant[6] == 0 || (g_variant[6] >= 10 && g_variant[6] <= 39))
       return launch_conv3x3s2_x(a, g_variant[6] == 0 ? 0 : g_variant[6] - 10, s, kname);
   }
   if (a.Hout == 32) {

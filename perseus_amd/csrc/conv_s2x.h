@@ -20,21 +20,34 @@
 // X3 (fp16x3 parity mode): activation / weight hi-lo planes and 3 virtual blocks per
 // 64-channel block, as conv_gx.h's X3; the downsample's weights carry their own
 // per-channel power-of-2 scale (scale2).
+//
+// TPW > 1: one workgroup runs TPW spatial tiles (same output channels, same image) as
+// ONE step stream: the weight ring runs on across the tile boundary, the next tile's
+// first patch is DMA'd during the current tile's K loop like any next block's patch, and
+// a tile's output stores open the next tile's first step (counted in the vmcnt plan:
+// loads, stores and LDS-DMA retire in issue order).  At B = 64 the layer2 / layer3
+// entries have two workgroups' worth of tiles per CU; as two rounds of workgroups each
+// round paid the patch + weight prologue and the store drain (3.7 + 1.8 us of 10 on
+// layer2).  Bias / scales are loaded in the prologue (one set for all tiles).
 #pragma once
 #include "conv_gx.h"
 
 namespace pa {
 
 // DBG = 4: s_memrealtime stamps into a.trace (conv.h trace_stamp: 0 start, 1 prologue landed,
-// 2 K loop done, 3 epilogue stores issued, 63 stores retired)
-template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G, bool WT = true, bool X3 = false, int DBG = 0>
+// 2 K loop done, 3 epilogue stores issued, 63 stores retired; TPW > 1: 4 + j tile j + 1's
+// first step)
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G, bool WT = true, bool X3 = false, int DBG = 0,
+          int TPW = 1>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
   using VB = GxBlocks<X3, NCB>;
   constexpr int XS = X3 ? 2 : 1;
   constexpr int SPB = 10;  // 9 taps + downsample per 64-channel block
-  constexpr int NSTEPS = VB::NVB * SPB;
+  constexpr int SPT = VB::NVB * SPB;  // steps per tile
+  constexpr int NBLK = TPW * VB::NVB;  // patch blocks in the stream
+  constexpr int NSTEPS = TPW * SPT;
   constexpr int KW = XS * CIN;
   constexpr int KTOT = 9 * KW;
   constexpr int PH = 2 * TH + 1;
@@ -43,7 +56,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   constexpr int NPC = (NP * 8 + 63) / 64 * 64;
   constexpr int PDMA = NPC / 64 / NW + (NPC / 64 % NW ? 1 : 0);
   constexpr int PATCHB = (PDMA * NW * 64) * 16;
-  constexpr int NPB = VB::NVB > 1 ? 2 : 1;  // patch buffers
+  constexpr int NPB = NBLK > 1 ? 2 : 1;  // patch buffers
   constexpr int WB = BN * 128;
   constexpr int WDMA = BN * 8 / NT;
   constexpr int BM = TH * TW;
@@ -54,9 +67,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile");
   static_assert(G >= 1 && G <= 3 && PD >= G + 1 && PD <= 8, "prefetch distance / steps per barrier");
   constexpr int NSLOT = PD + G;
-  constexpr int RL = 2 * XS * TN;  // epilogue loads: bias, bias2 (+ scale, scale2)
+  constexpr int RL = TPW > 1 ? 0 : 2 * XS * TN;  // epilogue loads in the stream: bias, bias2 (+ scale, scale2)
   constexpr int RSD = 4;
-  constexpr GxPlan plan{NSTEPS, VB::NVB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, SPB};
+  constexpr int NST = TM * (TN / 2) * 2 * XS;  // output stores per tile (out, out2; hi, lo)
+  constexpr GxPlan plan{NSTEPS, NBLK, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, SPB,
+                        TPW > 1 ? SPT : 0, NST};
   static_assert(NPB * PATCHB + NSLOT * WB <= 163840, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[NPB * PATCHB + NSLOT * WB];
   char* patch = smem;
@@ -71,7 +86,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   const _Float16* __restrict__ wds = (const _Float16*)a.wds;
 
   const int ntn = Cout / BN;
-  int tn_idx, sp;
+  int tn_idx, sp;  // sp: the workgroup's group of TPW consecutive spatial tiles
   if (xg) {  // blocks b and b + 8 share an XCD: the N-tiles of one spatial tile there
     const int b = blockIdx.x, x8 = b & 7, i = b >> 3;
     tn_idx = i % ntn;
@@ -82,29 +97,32 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   }
   if constexpr (DBG == 4) trace_stamp(a.trace, 0);
   const int tw_n = W / TW, tpi = (H / TH) * tw_n;
-  const int img = sp / tpi;
-  const int rem = sp - img * tpi;
-  const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
+  const int img = (sp * TPW) / tpi;  // one image per group (tpi % TPW == 0)
+  if (img >= a.B) return;
   const int n0 = tn_idx * BN;
+  auto tile_origin = [&](int j, int& th0, int& tw0) __attribute__((always_inline)) {
+    const int rem = sp * TPW + j - img * tpi;
+    th0 = (rem / tw_n) * TH;
+    tw0 = (rem - (rem / tw_n) * tw_n) * TW;
+  };
 
   // patch DMA: LDS slot c = (i * NW + wid) * 64 + lane holds position p = c >> 3,
-  // logical chunk (c & 7) ^ swizzle(p)
-  const char* psrc[PDMA];
-#pragma unroll
-  for (int i = 0; i < PDMA; ++i) {
-    const int c = (i * NW + wid) * 64 + lane;
-    const int p = c >> 3, pc = c & 7;
-    const int lc = pc ^ ((p >> 1) & 7);
-    const int pr = p / PW, pos = p - (p / PW) * PW;
-    const int col = pos <= TW ? 2 * pos : 2 * (pos - TW - 1) + 1;
-    const int h = 2 * th0 - 1 + pr, x = 2 * tw0 - 1 + col;
-    const bool ok = p < NP && pos < 2 * TW + 1 && img < a.B && (unsigned)h < (unsigned)Hin && (unsigned)x < (unsigned)Win;
-    psrc[i] = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * KW + lc * 8) : nullptr;
-  }
-  auto dma_patch = [&](int vb, int buf) __attribute__((always_inline)) {
+  // logical chunk (c & 7) ^ swizzle(p); block blk = tile j's virtual block vb
+  auto dma_patch = [&](int blk, int buf) __attribute__((always_inline)) {
+    const int j = blk / VB::NVB, vb = blk - (blk / VB::NVB) * VB::NVB;
+    int th0, tw0;
+    tile_origin(j, th0, tw0);
 #pragma unroll
     for (int i = 0; i < PDMA; ++i) {
-      const char* s = psrc[i] ? psrc[i] + VB::pblk(vb) * 128 : (const char*)gx_zero_line;
+      const int c = (i * NW + wid) * 64 + lane;
+      const int p = c >> 3, pc = c & 7;
+      const int lc = pc ^ ((p >> 1) & 7);
+      const int pr = p / PW, pos = p - (p / PW) * PW;
+      const int col = pos <= TW ? 2 * pos : 2 * (pos - TW - 1) + 1;
+      const int h = 2 * th0 - 1 + pr, x = 2 * tw0 - 1 + col;
+      const bool ok = p < NP && pos < 2 * TW + 1 && (unsigned)h < (unsigned)Hin && (unsigned)x < (unsigned)Win;
+      const char* s = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * KW + lc * 8) + VB::pblk(vb) * 128
+                         : (const char*)gx_zero_line;
       xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
     }
   };
@@ -119,7 +137,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     dsrc[i] = wds + (size_t)(n0 + xperm(co)) * KW + lc * 8;
   }
   auto dma_w = [&](int s) __attribute__((always_inline)) {
-    const int vb = s / SPB, t = s % SPB;
+    const int vb = (s % SPT) / SPB, t = s % SPB;
     const int wb = VB::wblk(vb) * 64;
 #pragma unroll
     for (int i = 0; i < WDMA; ++i) {
@@ -130,13 +148,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
 
   const int o = xfrag(r16);
   int ppix[TM];  // LDS position of tap (0, 0) for this lane's pixel of fragment tm
-  size_t pixo[TM];
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     const int m = wm * WTM + tm * 16 + o;
     const int y = m / TW, x = m - (m / TW) * TW;
     ppix[tm] = 2 * y * PW + x;
-    pixo[tm] = (((size_t)(img < a.B ? img : 0) * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
   }
   f32x4 bias[TN], bias2[TN];
   f32x4 scl[X3 ? TN : 1], scl2[X3 ? TN : 1];
@@ -166,9 +182,48 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
 #pragma unroll
   for (int t = 0; t < PD; ++t)
     if (t < NSTEPS) dma_w(t);
+  if constexpr (TPW > 1) load_epi();
   xwait_vm<0>();
   __builtin_amdgcn_s_barrier();
   if constexpr (DBG == 4) trace_stamp(a.trace, 1);
+
+  _Float16* __restrict__ out = (_Float16*)a.out;
+  _Float16* __restrict__ out2 = (_Float16*)a.out2;
+  auto epilogue = [&](int j) __attribute__((always_inline)) {
+    int th0, tw0;
+    tile_origin(j, th0, tw0);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int m = wm * WTM + tm * 16 + o;
+      const int y = m / TW, x = m - (m / TW) * TW;
+      const size_t pixo = (((size_t)img * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
+#pragma unroll
+      for (int p = 0; p < TN / 2; ++p) {
+        half8 h1, h2, l1, l2;
+#pragma unroll
+        for (int e8 = 0; e8 < 8; ++e8) {
+          const int tn = 2 * p + (e8 >> 2), e = e8 & 3;
+          if constexpr (X3) {
+            const HiLo a1 = split_x3(fmaxf(acc[tm][tn][e] * scl[tn][e] + bias[tn][e], 0.f));
+            const HiLo a2 = split_x3(accd[tm][tn][e] * scl2[tn][e] + bias2[tn][e]);
+            h1[e8] = a1.hi;
+            l1[e8] = a1.lo;
+            h2[e8] = a2.hi;
+            l2[e8] = a2.lo;
+          } else {
+            h1[e8] = (_Float16)fmaxf(acc[tm][tn][e] + bias[tn][e], 0.f);
+            h2[e8] = (_Float16)(accd[tm][tn][e] + bias2[tn][e]);
+          }
+        }
+        store16<WT>(out, (unsigned)((pixo + p * 32) * 2), h1);
+        store16<WT>(out2, (unsigned)((pixo + p * 32) * 2), h2);
+        if constexpr (X3) {
+          store16<WT>(out, (unsigned)((pixo + Cout + p * 32) * 2), l1);
+          store16<WT>(out2, (unsigned)((pixo + Cout + p * 32) * 2), l2);
+        }
+      }
+    }
+  };
 
   xu4 fa[2][TN], fb[2][TM];
   auto read_frags = [&](auto kc) __attribute__((always_inline)) {
@@ -202,6 +257,18 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     constexpr int S = decltype(sc)::value;
     constexpr int CB = S / SPB;
     using DS = std::integral_constant<bool, S % SPB == 9>;
+    if constexpr (S > 0 && S % SPT == 0) {  // previous tile done: its stores (plan.ns), fresh accumulators
+      if constexpr (DBG == 4) trace_stamp(a.trace, 3 + S / SPT);
+      epilogue(S / SPT - 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          accd[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     read_frags(xic<2 * S + 1>{});
     __builtin_amdgcn_s_setprio(1);
     mfma(xic<0>{}, DS{});
@@ -210,8 +277,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     // DMAs after this step's LDS reads (see xdma16); order = GxPlan's
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + PD < NSTEPS) dma_w(S + PD);
-    if constexpr (CB + 1 < VB::NVB && S == plan.ps(CB + 1)) dma_patch(CB + 1, (CB + 1) & 1);
-    if constexpr (S == plan.rs) {
+    if constexpr (CB + 1 < NBLK && S == plan.ps(CB + 1)) dma_patch(CB + 1, (CB + 1) & 1);
+    if constexpr (TPW == 1 && S == plan.rs) {
       __builtin_amdgcn_sched_barrier(0);
       load_epi();
     }
@@ -227,37 +294,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   });
   if constexpr (DBG == 4) trace_stamp(a.trace, 2);
   xwait_vm<0>();
-
-  if (img >= a.B) return;
-  _Float16* __restrict__ out = (_Float16*)a.out;
-  _Float16* __restrict__ out2 = (_Float16*)a.out2;
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-    for (int p = 0; p < TN / 2; ++p) {
-      half8 h1, h2, l1, l2;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int tn = 2 * p + (j >> 2), e = j & 3;
-        if constexpr (X3) {
-          const HiLo a1 = split_x3(fmaxf(acc[tm][tn][e] * scl[tn][e] + bias[tn][e], 0.f));
-          const HiLo a2 = split_x3(accd[tm][tn][e] * scl2[tn][e] + bias2[tn][e]);
-          h1[j] = a1.hi;
-          l1[j] = a1.lo;
-          h2[j] = a2.hi;
-          l2[j] = a2.lo;
-        } else {
-          h1[j] = (_Float16)fmaxf(acc[tm][tn][e] + bias[tn][e], 0.f);
-          h2[j] = (_Float16)(accd[tm][tn][e] + bias2[tn][e]);
-        }
-      }
-      store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), h1);
-      store16<WT>(out2, (unsigned)((pixo[tm] + p * 32) * 2), h2);
-      if constexpr (X3) {
-        store16<WT>(out, (unsigned)((pixo[tm] + Cout + p * 32) * 2), l1);
-        store16<WT>(out2, (unsigned)((pixo[tm] + Cout + p * 32) * 2), l2);
-      }
-    }
+  epilogue(TPW - 1);
   if constexpr (DBG == 4) {
     trace_stamp(a.trace, 3);
     __builtin_amdgcn_s_waitcnt(0);
@@ -266,7 +303,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
 }
 
 template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1, bool WT = true, bool X3 = false,
-          int DBG = 0>
+          int DBG = 0, int TPW = 1>
 static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
   PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "s2x conv: output over 2 GB");
   PA_CHECK(!X3 || (a.scale && a.scale2), "s2x conv (fp16x3): scales required");
@@ -274,11 +311,13 @@ static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
   PA_CHECK(a.Hin == 2 * a.Hout && a.Win == 2 * a.Wout, "s2x conv: %dx%d -> %dx%d", a.Hin, a.Win, a.Hout, a.Wout);
   PA_CHECK(a.Hout % TH == 0 && a.Wout % TW == 0, "s2x conv: %dx%d not tiled by %dx%d", a.Hout, a.Wout, TH, TW);
   PA_CHECK(a.Cout % BN == 0, "s2x conv: Cout %d %% BN %d", a.Cout, BN);
+  PA_CHECK((a.Hout / TH) * (a.Wout / TW) % TPW == 0, "s2x conv: %d tiles per image not grouped by %d",
+           (a.Hout / TH) * (a.Wout / TW), TPW);
   const int ntn = a.Cout / BN;
-  const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW);
+  const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW) / TPW;  // groups of TPW tiles
   const int x = xg && nsp % 8 == 0;
-  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT, X3, DBG>), dim3(nsp * ntn), dim3(WM * WN * 64),
-                     0, s, a, x);
+  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT, X3, DBG, TPW>), dim3(nsp * ntn),
+                     dim3(WM * WN * 64), 0, s, a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

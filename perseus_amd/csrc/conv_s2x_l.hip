@@ -1,6 +1,6 @@
 // conv_s2x.h instantiations: the stride-2 + downsample entry conv of layers 2-4.
 // variant & 3 selects the tile / prefetch configuration, variant & 4 turns the
-// XCD-aware block order off.
+// XCD-aware block order off; 16.. are the multi-tile (TPW) workgroups.
 #include "conv_s2x.h"
 
 namespace pa {
@@ -9,20 +9,26 @@ int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const ch
   if (a.B <= 0) return PA_OK;
   const bool xg = !(variant & 4);
   if (a.Hout == 32 && a.Cin == 64) {
+    // shipped: 4x16 x 128 tiles, 4 per workgroup as one step stream (19.9 vs 21.1 us for
+    // one 8x16 tile per workgroup in two rounds; tools/layer_ab.py, r02)
     if (kname) *kname = "conv3x3s2x_l2";
-    if (variant & 8) return run_s2x<8, 16, 128, 4, 2, 64, 3, 1, false>(a, xg, s);  // plain (write-back) stores
-    if (variant == 7 && a.trace) return run_s2x<8, 16, 128, 4, 2, 64, 3, 1, true, false, 4>(a, xg, s);  // timestamps
+    if (variant & 8) return run_s2x<4, 16, 128, 2, 4, 64, 4, 1, false, false, 0, 4>(a, true, s);  // plain stores
+    if (variant == 7 && a.trace) return run_s2x<4, 16, 128, 2, 4, 64, 4, 1, true, false, 4, 4>(a, true, s);  // timestamps
+    if (variant == 19 && a.trace) return run_s2x<8, 16, 128, 4, 2, 64, 3, 1, true, false, 4>(a, xg, s);
+    if (variant == 16) return run_s2x<4, 16, 128, 2, 2, 64, 3, 1, true, false, 0, 4>(a, true, s);  // 4 waves of 32x64
+    if (variant == 17) return run_s2x<4, 16, 128, 2, 4, 64, 3, 1, true, false, 0, 4>(a, true, s);  // distance 3
     switch (variant & 3) {
-      case 1: return run_s2x<8, 16, 128, 4, 2, 64, 3, 2>(a, xg, s);
+      case 1: return run_s2x<8, 16, 128, 4, 2, 64, 3>(a, xg, s);  // one 8x16 tile per workgroup (round-1/2 kernel)
       case 2: return run_s2x<8, 16, 64, 4, 1, 64, 3>(a, xg, s);
       case 3: return run_s2x<4, 16, 128, 2, 2, 64, 3>(a, xg, s);
-      default: return run_s2x<8, 16, 128, 4, 2, 64, 3>(a, xg, s);
+      default: return run_s2x<4, 16, 128, 2, 4, 64, 4, 1, true, false, 0, 4>(a, xg, s);
     }
   }
   if (a.Hout == 16 && a.Cin == 128) {
     if (kname) *kname = "conv3x3s2x_l3";
     if (variant & 8) return run_s2x<4, 16, 128, 2, 4, 128, 3, 1, false>(a, xg, s);  // plain (write-back) stores
     if (variant == 7 && a.trace) return run_s2x<4, 16, 128, 2, 4, 128, 3, 1, true, false, 4>(a, xg, s);  // timestamps
+    if (variant == 17) return run_s2x<4, 16, 128, 2, 2, 128, 3, 1, true, false, 0, 2>(a, true, s);  // 19.9 vs 18.4 us
     switch (variant & 3) {
       case 1: return run_s2x<4, 16, 128, 2, 4, 128, 3, 2>(a, xg, s);
       case 2: return run_s2x<4, 16, 64, 2, 2, 128, 4>(a, xg, s);

@@ -257,6 +257,9 @@ def test_kernel_variants_agree_bit_for_bit(B):
         ((1, 30), (7, 1)),  # layer1: register-staged kernel on every conv; the generic head
         ((1, 32),),  # layer1: the one-tile patch kernel (independent of the shipped LDS-DMA kernel)
         ((7, 3),),  # avgpool + fc fused into layer4's last conv instead of head_fp16
+        ((6, 11),),  # stride-2 entries: one tile per workgroup (layer2: the round-2a 8x16 kernel)
+        ((6, 26),),  # multi-tile workgroups: layer2 4 waves of 32x64; layer3 as shipped
+        ((6, 27),),  # layer2 prefetch distance 3; layer3 two 4x16 tiles per workgroup
     )
     for vs in sets:
         try:
