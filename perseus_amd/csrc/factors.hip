@@ -518,14 +518,20 @@ __global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restric
 // straight from the detector output y (normalized, denormalized here exactly as
 // kornia's denormalize_pixel_coordinates in f32, common.h kornia_denorm).
 //
-// One wave (workgroup) per 64 consecutive factors of one kind (traj_all_kernel below).
-// Outputs are staged per wave in LDS and written as the
-// wave's contiguous slice of each output array, 16 B per lane per store (a lane's own
-// record is 16-288 B of column-major doubles: stored directly, one wave-store instruction
-// would scatter over the whole 1-18 KB slice).
+// Workgroups of two waves.  A dynamics workgroup takes 64 consecutive PoseDynamicsFactors
+// and splits each factor's work between its waves (below); every other workgroup runs two
+// independent 64-factor units (projection, then constant-velocity).  Outputs are staged
+// per wave in LDS and written as the wave's contiguous slice of each output array, 16 B
+// per lane per store (a lane's own record is 16-288 B of column-major doubles: stored
+// directly, one wave-store instruction would scatter over the whole 1-18 KB slice).
 namespace trj {
-constexpr int STAGE = 64 * 60;  // doubles: dynamics r + J0 + J1 (phase A) / J2 + J3 + err (phase B)
-}
+// doubles: dynamics wave 0 staging (r | J3 | err, then J0); A, handed from wave 0 to
+// wave 1, whose slots then stage wave 1's J1 and J2; dtw's upper block handed back.
+// 35 KB: four workgroups per CU, the two-waves-per-SIMD register limit
+constexpr int W0 = 0, XA = 64 * 43, W1 = XA, XD = XA + 64 * 18, STAGE = XD + 64 * 9;
+constexpr int UNIT = 64 * 22;  // projection / constant-velocity staging per wave
+static_assert(2 * UNIT <= STAGE, "unit staging");
+}  // namespace trj
 
 // the wave's n records of `per` doubles, staged at st[lane * per ..], -> dst[0 .. n * per)
 __device__ __forceinline__ void wave_flush(double* __restrict__ dst, const double* st, int n, int per) {
@@ -540,49 +546,162 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ dst, const doubl
   }
 }
 
-__device__ __forceinline__ void traj_dyn_wave(const pa_traj_args& a, long w, double* st) {
-  const int lane = threadIdx.x;
-  const long nd = (long)a.T * (a.L - 1);
-  auto sync = [] { lds_barrier(); };  // LDS only: the flushed stores stay in flight
-  {  // PoseDynamicsFactor (l, l+1)
-    const long j0 = w * 64;
-    const int n = (int)(nd - j0 < 64 ? nd - j0 : 64);
-    const long jd = j0 + (lane < n ? lane : n - 1);  // tail lanes recompute the last factor, store nothing
-    const long t = jd / (a.L - 1), f = t * a.L + (jd - t * (a.L - 1));
-    double* sr = st + lane * 6;
-    double* s0 = st + 64 * 6 + lane * 36;
-    double* s1 = st + 64 * 42 + lane * 18;
-    double* s2 = st + lane * 18;
-    double* s3 = st + 64 * 18 + lane * 36;
-    double* se = st + 64 * 54 + lane;
-    const bool J = a.j_dyn0 || a.j_dyn1 || a.j_dyn2 || a.j_dyn3;
-    auto mid = [&] {  // r, J0, J1 staged: write them out, free the buffer
-      sync();
-      wave_flush(a.r_dyn + j0 * 6, st, n, 6);
-      if (a.j_dyn0) wave_flush(a.j_dyn0 + j0 * 36, st + 64 * 6, n, 36);
-      if (a.j_dyn1) wave_flush(a.j_dyn1 + j0 * 18, st + 64 * 42, n, 18);
-      sync();
-    };
-    dyn_one(a.pose + f * 12, a.angvel + f * 3, a.vel + f * 3, a.pose + (f + 1) * 12, a.dt, a.vel_frame, a.isig_dyn,
-            sr, a.j_dyn0 ? s0 : nullptr, a.j_dyn1 ? s1 : nullptr, a.j_dyn2 ? s2 : nullptr, a.j_dyn3 ? s3 : nullptr,
-            a.err_dyn ? se : nullptr, mid);
-    sync();
-    if (J) {
-      if (a.j_dyn2) wave_flush(a.j_dyn2 + j0 * 18, st, n, 18);
-      if (a.j_dyn3) wave_flush(a.j_dyn3 + j0 * 36, st + 64 * 18, n, 36);
+// wave-local LDS ordering: the staging of one wave is written and flushed by that wave only
+__device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// 6 x 3 column-major block of a Jacobian: rows 0..2 from `top` (zero if !has_top), rows
+// 3..5 from `bot`, row-scaled by sw (references, not pointers: an address-taken M3 lives
+// in scratch)
+__device__ __forceinline__ void stage6x3(double* J, bool has_top, const M3& top, const M3& bot, const double* sw) {
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      J[c * 6 + r] = (has_top ? top(r, c) : 0.0) * sw[r];
+      J[c * 6 + 3 + r] = bot(r, c) * sw[3 + r];
     }
-    if (a.err_dyn) wave_flush(a.err_dyn + j0, st + 64 * 54, n, 1);
+}
+
+// PoseDynamicsFactor (l, l+1), 64 per workgroup, factor k on lane k of BOTH waves:
+//   wave 0: Expmap -> compose -> between -> Logmap (r), dlog = LogmapDerivative(rel),
+//           A = -dlog Ad(rel^-1), H0 = A Ad(inc^-1); writes r, J3, err, J0
+//   wave 1: ExpmapDerivative(xi) = [[dexp, 0], [Q(xw, xv), dexp]] -- independent of the
+//           chain, so it runs beside it on another SIMD -- then dtw = dt A D; writes J1, J2
+// A goes 0 -> 1 and dtw's upper block 1 -> 0 (world-frame J0) through LDS, one barrier
+// each.  The products and their order are dyn_one's (factors.py:54-142), so the values
+// are the same; wave 0's chain is one Barfoot Q, one rot_dexp, one 6x6 product and the
+// J1 / J2 work shorter.
+__device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, double* st) {
+  using namespace trj;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long nd = (long)a.T * (a.L - 1);
+  const long j0 = blk * 64;
+  const int n = (int)(nd - j0 < 64 ? nd - j0 : 64);
+  const long jd = j0 + (lane < n ? lane : n - 1);  // tail lanes recompute the last factor, store nothing
+  const long t = jd / (a.L - 1), f = t * a.L + (jd - t * (a.L - 1));
+  const bool J = a.j_dyn0 || a.j_dyn1 || a.j_dyn2 || a.j_dyn3;
+  const bool world = a.vel_frame == PA_VEL_WORLD;
+  const double dt = a.dt;
+  double sw[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sw[i] = a.isig_dyn ? a.isig_dyn[i] : 1.0;
+  const Pose T1 = load_pose(a.pose + f * 12);
+  const V3 w = load3(a.angvel + f * 3);
+  V3 vb = load3(a.vel + f * 3);
+  if (world) vb = mtv(T1.R, vb);  // transformTo / unrotate (factors.py:100,134)
+  const V3 xw = dt * w, xv = dt * vb;
+  const Ang ax = ang(xw);  // |xi_w| for Expmap, ExpmapDerivative and Q
+  double* XAp = st + XA + lane * 18;
+  double* XDp = st + XD + lane * 9;
+  if (wv == 0) {
+    const Pose T2 = load_pose(a.pose + (f + 1) * 12);
+    const Pose inc = pose_exp(xw, xv, ax);          // Expmap (:104 / :136)
+    const Pose pred = compose(T1, inc);             // compose (:105)
+    const Pose rel = compose(inverse(pred), T2);    // between (:108)
+    V3 ew, ev;
+    pose_log(rel, ew, ev);  // Logmap (:109)
+    const double r[6] = {ew.x, ew.y, ew.z, ev.x, ev.y, ev.z};
+    double e = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) e += (r[i] * sw[i]) * (r[i] * sw[i]);
+    BL dlog{}, A{};
+    if (J) {
+      // dlog = LogmapDerivative(rel) (:112)
+      const Ang ae = ang(ew);
+      const M3 Jw = rot_dlog(ew, ae);
+      dlog = BL{Jw, scale(mul(mul(Jw, compute_q(ew, ev, ae)), Jw), -1.0)};
+      // A = dlog * drel_dpred, drel_dpred = -Ad(rel^-1)
+      A = mulbl(dlog, adjoint_bl(inverse(rel)));
+      A.A = scale(A.A, -1.0);
+      A.C = scale(A.C, -1.0);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        XAp[i] = A.A.a[i];
+        XAp[9 + i] = A.C.a[i];
+      }
+    }
+    lds_barrier();  // A -> wave 1
+    // phase 1, while wave 1 forms dtw: r | J3 = dlog * I (:130) | err
+    double* sr = st + W0 + lane * 6;
+    double* s3 = st + W0 + 64 * 6 + lane * 36;
+    double* se = st + W0 + 64 * 42 + lane;
+    if (lane < n) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) sr[i] = r[i] * sw[i];
+      *se = 0.5 * e;
+      if (a.j_dyn3) {
+        stage6x3(s3, true, dlog.A, dlog.C, sw);
+        stage6x3(s3 + 18, false, dlog.A, dlog.A, sw);
+      }
+    }
+    BL H0{};
+    if (J) H0 = mulbl(A, adjoint_bl(inverse(inc)));  // H0 = A * Ad(inc^-1)
+    wave_sync();
+    wave_flush(a.r_dyn + j0 * 6, st + W0, n, 6);
+    if (a.j_dyn3) wave_flush(a.j_dyn3 + j0 * 36, st + W0 + 64 * 6, n, 36);
+    if (a.err_dyn) wave_flush(a.err_dyn + j0, st + W0 + 64 * 42, n, 1);
+    lds_barrier();  // dtw's upper block <- wave 1; wave 0's phase-1 reads are done
+    if (a.j_dyn0) {
+      // J0 = H0 (+ world frame: lower-left += dtw[3:, 3:] skew(vb), :122); columns 3..5 [0; H0.A]
+      M3 C0 = H0.C;
+      if (world) {
+        M3 dA;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) dA.a[i] = XDp[i];
+        C0 = add(H0.C, mul(dA, skew(vb)));
+      }
+      double* s0 = st + W0 + lane * 36;
+      if (lane < n) {
+        stage6x3(s0, true, H0.A, C0, sw);
+        stage6x3(s0 + 18, false, H0.A, H0.A, sw);
+      }
+      wave_sync();
+      wave_flush(a.j_dyn0 + j0 * 36, st + W0, n, 36);
+    }
+  } else {
+    BL D{};
+    if (J) D = BL{rot_dexp(xw, ax), compute_q(xw, xv, ax)};  // ExpmapDerivative(xi)
+    lds_barrier();  // A <- wave 0
+    BL dtw{};
+    if (J) {
+      BL A;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        A.A.a[i] = XAp[i];
+        A.C.a[i] = XAp[9 + i];
+      }
+      // derr_dtwist = dt * dlog * drel_dpred * I * ExpmapDerivative(xi) (:117)
+      dtw = mulbl(A, D);
+      dtw.A = scale(dtw.A, dt);
+      dtw.C = scale(dtw.C, dt);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) XDp[i] = dtw.A.a[i];
+    }
+    lds_barrier();  // dtw's upper block -> wave 0
+    double* s1 = st + W1 + lane * 18;
+    if (a.j_dyn1) {  // dtw[:, :3] (:117-118)
+      if (lane < n) stage6x3(s1, true, dtw.A, dtw.C, sw);
+      wave_sync();
+      wave_flush(a.j_dyn1 + j0 * 18, st + W1, n, 18);
+      wave_sync();
+    }
+    if (a.j_dyn2) {  // J2 = dtw[:, 3:] @ R1^T (world, :125) or dtw[:, 3:] (body, :128); dtw[:3, 3:] = 0
+      if (lane < n) stage6x3(s1, false, dtw.A, world ? mul(dtw.A, tr(T1.R)) : dtw.A, sw);
+      wave_sync();
+      wave_flush(a.j_dyn2 + j0 * 18, st + W1, n, 18);
+    }
   }
 }
 
-__device__ __forceinline__ void traj_proj_wave(const pa_traj_args& a, long w, double* st) {
-  const int lane = threadIdx.x;
+// one 64-factor projection (unit < wp) or constant-velocity unit, staged in this wave's
+// own LDS region (wave-local syncs only)
+__device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, double* st) {
+  const int lane = threadIdx.x & 63;
   const long F = (long)a.T * a.L;
   const long np = F * a.n_kp, nd = (long)a.T * (a.L - 1);
   const long wp = (np + 63) / 64;
-  auto sync = [] { lds_barrier(); };  // LDS only: the flushed stores stay in flight
-  if (w < wp) {  // KeypointProjectionFactor, factor i = f * K + k
-    const long i0 = w * 64;
+  if (u < wp) {  // KeypointProjectionFactor, factor i = f * K + k
+    const long i0 = u * 64;
     const int n = (int)(np - i0 < 64 ? np - i0 : 64);
     const long i = i0 + (lane < n ? lane : n - 1);
     const long f = i / a.n_kp;
@@ -594,42 +713,46 @@ __device__ __forceinline__ void traj_proj_wave(const pa_traj_args& a, long w, do
     proj_one(a.pose + f * 12, load3(a.corners + 3 * k), (double)px, (double)py, a.K, a.tcam, a.isig_proj,
              st + lane * 2, a.j_proj ? st + 64 * 2 + lane * 12 : nullptr, a.err_proj ? st + 64 * 14 + lane : nullptr,
              sst + lane);
-    sync();
+    wave_sync();
     wave_flush(a.r_proj + i0 * 2, st, n, 2);
     if (a.j_proj) wave_flush(a.j_proj + i0 * 12, st + 64 * 2, n, 12);
     if (a.err_proj) wave_flush(a.err_proj + i0, st + 64 * 14, n, 1);
     if (a.status && lane < n) a.status[i0 + lane] = sst[lane];
     return;
   }
-  const long c0 = (w - wp) * 64;  // ConstantVelocityFactor (l, l+1)
+  const long c0 = (u - wp) * 64;  // ConstantVelocityFactor (l, l+1)
   if (c0 >= nd) return;
   const int n = (int)(nd - c0 < 64 ? nd - c0 : 64);
   const long jc = c0 + (lane < n ? lane : n - 1);
   const long t = jc / (a.L - 1), f = t * a.L + (jc - t * (a.L - 1));
   cv_one(a.vel + f * 3, a.vel + (f + 1) * 3, a.isig_cv, st + lane * 3, a.j_cv0 ? st + 64 * 3 + lane * 9 : nullptr,
          a.j_cv1 ? st + 64 * 12 + lane * 9 : nullptr, a.err_cv ? st + 64 * 21 + lane : nullptr);
-  sync();
+  wave_sync();
   wave_flush(a.r_cv + c0 * 3, st, n, 3);
   if (a.j_cv0) wave_flush(a.j_cv0 + c0 * 9, st + 64 * 3, n, 9);
   if (a.j_cv1) wave_flush(a.j_cv1 + c0 * 9, st + 64 * 12, n, 9);
   if (a.err_cv) wave_flush(a.err_cv + c0, st + 64 * 21, n, 1);
 }
 
-// one launch, the dynamics waves dispatched first: they hold the longest per-lane
+// one launch, the dynamics workgroups dispatched first: they hold the longest per-lane
 // chains and the projection / constant-velocity waves fill the other SIMDs meanwhile.
-// Two waves per SIMD (the dynamics code then spills 76 B per lane to scratch: 16.1 us at
-// 1000 x 24, against 17.8 at one wave per SIMD); block-lower-triangular 6x6 products in
-// the dynamics Jacobians (19.0 -> 17.8 us).  Also measured: two launches (the projection
-// kernel at 76 VGPRs) 16.1 + 8.9 us; the dynamics launch on a forked side stream 42 us
-// (the cross-stream event round trips cost more than the overlap won); s_setprio on the
-// dynamics waves: no change.
-__global__ __launch_bounds__(64, 2) void traj_all_kernel(pa_traj_args a) {
+// Round 2a: one wave per 64 dynamics factors doing all of dyn_one, 16.1 us at 1000 x 24
+// (block-lower-triangular 6x6 products: 19.0 -> 17.8; two waves per SIMD 17.8 -> 16.1).
+// Also measured: two launches (the projection kernel at 76 VGPRs) 16.1 + 8.9 us; the
+// dynamics launch on a forked side stream 42 us; s_setprio on the dynamics waves: no
+// change; a lane PAIR per factor (both lanes running the shared chain, the Jacobian
+// halves as one instruction stream) 18.3 us.  This form: 15.3 us (dynamics workgroups
+// alone 12.7, projection / constant-velocity alone 11.3 at 45 KB of LDS per workgroup;
+// the 35 KB layout adds a fourth workgroup per CU).  Three waves per SIMD does not fit
+// (the compiler keeps 200 VGPRs).
+__global__ __launch_bounds__(128, 2) void traj_all_kernel(pa_traj_args a) {
   __shared__ __attribute__((aligned(16))) double st[trj::STAGE];
   const long wd = ((long)a.T * (a.L - 1) + 63) / 64;
   if ((long)blockIdx.x < wd) {
-    traj_dyn_wave(a, blockIdx.x, st);
+    traj_dyn_block(a, blockIdx.x, st);
   } else {
-    traj_proj_wave(a, blockIdx.x - wd, st);
+    const int wv = threadIdx.x >> 6;
+    traj_unit_wave(a, 2 * ((long)blockIdx.x - wd) + wv, st + wv * trj::UNIT);
   }
 }
 
@@ -669,7 +792,8 @@ int pa_trajectory_linearize(const pa_traj_args* a, void* stream) {
   PA_CHECK(a->r_proj && (a->L == 1 || (a->r_dyn && a->r_cv)), "null output pointer");
   PA_CHECK(a->vel_frame == PA_VEL_WORLD || a->vel_frame == PA_VEL_BODY, "vel_frame must be 'world' or 'body'.");
   const long np = (long)a->T * a->L * a->n_kp, nd = (long)a->T * (a->L - 1);
-  hipLaunchKernelGGL(pa::traj_all_kernel, dim3((unsigned)((np + 63) / 64 + 2 * ((nd + 63) / 64))), dim3(64), 0,
+  const long units = (np + 63) / 64 + (nd + 63) / 64;  // projection | constant-velocity, two per workgroup
+  hipLaunchKernelGGL(pa::traj_all_kernel, dim3((unsigned)((nd + 63) / 64 + (units + 1) / 2)), dim3(128), 0,
                      (hipStream_t)stream, *a);
   PA_LAUNCH_CHECK();
   return PA_OK;
