@@ -179,6 +179,10 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
       }
       mm(kc);
     });
+    if constexpr (DBG == 4) {  // per-wave K-loop end: slot 20 + 8 t + wave
+      if (lane == 0 && t < 5)
+        a.trace[blockIdx.x * TRACE_SLOTS + 20 + 8 * t + wid] = __builtin_amdgcn_s_memrealtime();
+    }
     xwait_vm<0>();  // next patch (+ residual)
 
     _Float16* __restrict__ out = (_Float16*)a.out;
