@@ -71,6 +71,14 @@ _SIGS = {
                                    C.c_void_p, C.c_void_p, C.c_void_p]),
     "pa_cv_linearize": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_void_p]),
+    # include/perseus_amd_loader.h (host pointers)
+    "pa_png_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "pa_png_decode": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_size_t]),
+    "pa_tiff_info": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "pa_tiff_decode_f32": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
+    "pa_load_keypoint_items": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                         C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                         C.c_void_p]),
 }
 
 PREC_FP16 = 0

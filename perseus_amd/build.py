@@ -2,7 +2,8 @@
 
     python -m perseus_amd.build [--force]
 
-Each csrc/*.hip is compiled to an object in parallel (perseus_amd/lib/obj/, kept for
+Each csrc/*.hip (hipcc) and csrc/*.cpp (host-only: g++) is compiled to an object in
+parallel (perseus_amd/lib/obj/, kept for
 incremental rebuilds: only sources newer than their object, or including a newer
 header, are recompiled), then linked into perseus_amd/lib/libperseus_amd.so
 (git-ignored, shipped to the GPU box with the snapshot).
@@ -31,8 +32,12 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mllvm", "-disable-promote-alloca-to-lds
 OBJDIR = os.path.join(LIBDIR, "obj")  # incremental build state (git- and gpurun-ignored)
 
 
+CXX = os.environ.get("CXX_HOST", "g++")
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", f"-I{os.path.join(ROOT, 'include')}"]
+
+
 def sources():
-    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
 def _deps():
@@ -48,6 +53,8 @@ def _includes(path, seen=None):
     with open(path) as fh:
         for name in _INC.findall(fh.read()):
             h = os.path.normpath(os.path.join(os.path.dirname(path), name))
+            if not os.path.exists(h):
+                h = os.path.join(ROOT, "include", name)
             if os.path.exists(h) and h not in seen:
                 seen.add(h)
                 _includes(h, seen)
@@ -55,7 +62,7 @@ def _includes(path, seen=None):
 
 
 def _obj(src: str) -> str:
-    return os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+    return os.path.join(OBJDIR, os.path.splitext(os.path.basename(src))[0] + ".o")
 
 
 def _stale(src: str) -> bool:
@@ -75,10 +82,13 @@ def up_to_date() -> bool:
 
 def _compile(src: str) -> str:
     obj = _obj(src)
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj + ".tmp"]
+    if src.endswith(".cpp"):
+        cmd = [CXX, *HOST_FLAGS, "-c", src, "-o", obj + ".tmp"]
+    else:
+        cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+        raise RuntimeError(f"{cmd[0]} failed for {src}:\n{r.stdout}\n{r.stderr}")
     os.replace(obj + ".tmp", obj)
     return obj
 
@@ -96,7 +106,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     objs = [_obj(s) for s in srcs]
     tmp = LIB + ".tmp"
     # -z defs: an unresolved symbol (e.g. a kernel stub the host pass dropped) fails the link
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-z,defs", "-o", tmp, *objs]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,-z,defs", "-o", tmp, *objs, "-lz"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
