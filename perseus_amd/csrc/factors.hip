@@ -525,10 +525,10 @@ __global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restric
 // per lane per store (a lane's own record is 16-288 B of column-major doubles: stored
 // directly, one wave-store instruction would scatter over the whole 1-18 KB slice).
 namespace trj {
-// doubles: dynamics wave 0 staging (r | J3 | err, then J0); A, handed from wave 0 to
-// wave 1, whose slots then stage wave 1's J1 and J2; dtw's upper block handed back.
-// 35 KB: four workgroups per CU, the two-waves-per-SIMD register limit
-constexpr int W0 = 0, XA = 64 * 43, W1 = XA, XD = XA + 64 * 18, STAGE = XD + 64 * 9;
+// doubles: dynamics wave 0 staging (r | J3 | err); A, handed from wave 0 to wave 1, whose
+// region then stages wave 1's J0, J1 and J2 in turn.  40 KB: four workgroups per CU, the
+// two-waves-per-SIMD register limit
+constexpr int W0 = 0, XA = 64 * 43, W1 = XA, STAGE = W1 + 64 * 36;
 constexpr int UNIT = 64 * 22;  // projection / constant-velocity staging per wave
 static_assert(2 * UNIT <= STAGE, "unit staging");
 }  // namespace trj
@@ -564,13 +564,12 @@ __device__ __forceinline__ void stage6x3(double* J, bool has_top, const M3& top,
 
 // PoseDynamicsFactor (l, l+1), 64 per workgroup, factor k on lane k of BOTH waves:
 //   wave 0: Expmap -> compose -> between -> Logmap (r), dlog = LogmapDerivative(rel),
-//           A = -dlog Ad(rel^-1), H0 = A Ad(inc^-1); writes r, J3, err, J0
-//   wave 1: ExpmapDerivative(xi) = [[dexp, 0], [Q(xw, xv), dexp]] -- independent of the
-//           chain, so it runs beside it on another SIMD -- then dtw = dt A D; writes J1, J2
-// A goes 0 -> 1 and dtw's upper block 1 -> 0 (world-frame J0) through LDS, one barrier
-// each.  The products and their order are dyn_one's (factors.py:54-142), so the values
-// are the same; wave 0's chain is one Barfoot Q, one rot_dexp, one 6x6 product and the
-// J1 / J2 work shorter.
+//           A = -dlog Ad(rel^-1); writes r, J3, err
+//   wave 1: Expmap(xi) and ExpmapDerivative(xi) = [[dexp, 0], [Q(xw, xv), dexp]] -- both
+//           independent of the chain, so they run beside it on another SIMD -- then, with A:
+//           dtw = dt A D and H0 = A Ad(inc^-1); writes J1, J2, J0
+// A goes 0 -> 1 through LDS (one barrier).  The products and their order are dyn_one's
+// (factors.py:54-142), so the values are the same; wave 0 holds only the chain and dlog.
 __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, double* st) {
   using namespace trj;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -591,27 +590,26 @@ __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, 
   if (world) vb = mtv(T1.R, vb);  // transformTo / unrotate (factors.py:100,134)
   const V3 xw = dt * w, xv = dt * vb;
   const Ang ax = ang(xw);  // |xi_w| for Expmap, ExpmapDerivative and Q
+  const Pose inc = pose_exp(xw, xv, ax);  // Expmap (:104 / :136)
   double* XAp = st + XA + lane * 18;
-  double* XDp = st + XD + lane * 9;
   if (wv == 0) {
     const Pose T2 = load_pose(a.pose + (f + 1) * 12);
-    const Pose inc = pose_exp(xw, xv, ax);          // Expmap (:104 / :136)
-    const Pose pred = compose(T1, inc);             // compose (:105)
-    const Pose rel = compose(inverse(pred), T2);    // between (:108)
+    const Pose pred = compose(T1, inc);           // compose (:105)
+    const Pose rel = compose(inverse(pred), T2);  // between (:108)
     V3 ew, ev;
     pose_log(rel, ew, ev);  // Logmap (:109)
     const double r[6] = {ew.x, ew.y, ew.z, ev.x, ev.y, ev.z};
     double e = 0.0;
 #pragma unroll
     for (int i = 0; i < 6; ++i) e += (r[i] * sw[i]) * (r[i] * sw[i]);
-    BL dlog{}, A{};
+    BL dlog{};
     if (J) {
       // dlog = LogmapDerivative(rel) (:112)
       const Ang ae = ang(ew);
       const M3 Jw = rot_dlog(ew, ae);
       dlog = BL{Jw, scale(mul(mul(Jw, compute_q(ew, ev, ae)), Jw), -1.0)};
       // A = dlog * drel_dpred, drel_dpred = -Ad(rel^-1)
-      A = mulbl(dlog, adjoint_bl(inverse(rel)));
+      BL A = mulbl(dlog, adjoint_bl(inverse(rel)));
       A.A = scale(A.A, -1.0);
       A.C = scale(A.C, -1.0);
 #pragma unroll
@@ -621,7 +619,7 @@ __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, 
       }
     }
     lds_barrier();  // A -> wave 1
-    // phase 1, while wave 1 forms dtw: r | J3 = dlog * I (:130) | err
+    // r | J3 = dlog * I (:130) | err
     double* sr = st + W0 + lane * 6;
     double* s3 = st + W0 + 64 * 6 + lane * 36;
     double* se = st + W0 + 64 * 42 + lane;
@@ -634,90 +632,107 @@ __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, 
         stage6x3(s3 + 18, false, dlog.A, dlog.A, sw);
       }
     }
-    BL H0{};
-    if (J) H0 = mulbl(A, adjoint_bl(inverse(inc)));  // H0 = A * Ad(inc^-1)
     wave_sync();
     wave_flush(a.r_dyn + j0 * 6, st + W0, n, 6);
     if (a.j_dyn3) wave_flush(a.j_dyn3 + j0 * 36, st + W0 + 64 * 6, n, 36);
     if (a.err_dyn) wave_flush(a.err_dyn + j0, st + W0 + 64 * 42, n, 1);
-    lds_barrier();  // dtw's upper block <- wave 1; wave 0's phase-1 reads are done
+  } else {
+    BL D{}, Ainc{};
+    if (J) {
+      D = BL{rot_dexp(xw, ax), compute_q(xw, xv, ax)};  // ExpmapDerivative(xi)
+      Ainc = adjoint_bl(inverse(inc));
+    }
+    lds_barrier();  // A <- wave 0
+    if (!J) return;
+    BL A;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      A.A.a[i] = XAp[i];
+      A.C.a[i] = XAp[9 + i];
+    }
+    // derr_dtwist = dt * dlog * drel_dpred * I * ExpmapDerivative(xi) (:117)
+    BL dtw = mulbl(A, D);
+    dtw.A = scale(dtw.A, dt);
+    dtw.C = scale(dtw.C, dt);
+    const BL H0 = mulbl(A, Ainc);  // H0 = A * Ad(inc^-1)
+    wave_sync();  // every lane has read its A slots: the region stages J0 / J1 / J2 next
+    double* s1 = st + W1;
     if (a.j_dyn0) {
       // J0 = H0 (+ world frame: lower-left += dtw[3:, 3:] skew(vb), :122); columns 3..5 [0; H0.A]
-      M3 C0 = H0.C;
-      if (world) {
-        M3 dA;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) dA.a[i] = XDp[i];
-        C0 = add(H0.C, mul(dA, skew(vb)));
-      }
-      double* s0 = st + W0 + lane * 36;
+      const M3 C0 = world ? add(H0.C, mul(dtw.A, skew(vb))) : H0.C;
       if (lane < n) {
-        stage6x3(s0, true, H0.A, C0, sw);
-        stage6x3(s0 + 18, false, H0.A, H0.A, sw);
+        stage6x3(s1 + lane * 36, true, H0.A, C0, sw);
+        stage6x3(s1 + lane * 36 + 18, false, H0.A, H0.A, sw);
       }
       wave_sync();
-      wave_flush(a.j_dyn0 + j0 * 36, st + W0, n, 36);
+      wave_flush(a.j_dyn0 + j0 * 36, s1, n, 36);
+      wave_sync();
     }
-  } else {
-    BL D{};
-    if (J) D = BL{rot_dexp(xw, ax), compute_q(xw, xv, ax)};  // ExpmapDerivative(xi)
-    lds_barrier();  // A <- wave 0
-    BL dtw{};
-    if (J) {
-      BL A;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        A.A.a[i] = XAp[i];
-        A.C.a[i] = XAp[9 + i];
-      }
-      // derr_dtwist = dt * dlog * drel_dpred * I * ExpmapDerivative(xi) (:117)
-      dtw = mulbl(A, D);
-      dtw.A = scale(dtw.A, dt);
-      dtw.C = scale(dtw.C, dt);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) XDp[i] = dtw.A.a[i];
-    }
-    lds_barrier();  // dtw's upper block -> wave 0
-    double* s1 = st + W1 + lane * 18;
     if (a.j_dyn1) {  // dtw[:, :3] (:117-118)
-      if (lane < n) stage6x3(s1, true, dtw.A, dtw.C, sw);
+      if (lane < n) stage6x3(s1 + lane * 18, true, dtw.A, dtw.C, sw);
       wave_sync();
-      wave_flush(a.j_dyn1 + j0 * 18, st + W1, n, 18);
+      wave_flush(a.j_dyn1 + j0 * 18, s1, n, 18);
       wave_sync();
     }
     if (a.j_dyn2) {  // J2 = dtw[:, 3:] @ R1^T (world, :125) or dtw[:, 3:] (body, :128); dtw[:3, 3:] = 0
-      if (lane < n) stage6x3(s1, false, dtw.A, world ? mul(dtw.A, tr(T1.R)) : dtw.A, sw);
+      if (lane < n) stage6x3(s1 + lane * 18, false, dtw.A, world ? mul(dtw.A, tr(T1.R)) : dtw.A, sw);
       wave_sync();
-      wave_flush(a.j_dyn2 + j0 * 18, st + W1, n, 18);
+      wave_flush(a.j_dyn2 + j0 * 18, s1, n, 18);
     }
   }
 }
 
-// one 64-factor projection (unit < wp) or constant-velocity unit, staged in this wave's
-// own LDS region (wave-local syncs only)
+// one projection unit of PPW x 64 factors (unit < wp: each lane evaluates PPW factors as
+// independent chains, so their loads overlap, then stages and flushes them 64 at a time) or
+// one 64-factor constant-velocity unit, staged in this wave's own LDS region (wave-local
+// syncs only)
+namespace trj {
+constexpr int PPW = 4;  // projection factors per lane
+}
 __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, double* st) {
+  using trj::PPW;
   const int lane = threadIdx.x & 63;
   const long F = (long)a.T * a.L;
   const long np = F * a.n_kp, nd = (long)a.T * (a.L - 1);
-  const long wp = (np + 63) / 64;
+  const long wp = (np + 64 * PPW - 1) / (64 * PPW);
   if (u < wp) {  // KeypointProjectionFactor, factor i = f * K + k
-    const long i0 = u * 64;
-    const int n = (int)(np - i0 < 64 ? np - i0 : 64);
-    const long i = i0 + (lane < n ? lane : n - 1);
-    const long f = i / a.n_kp;
-    const int k = (int)(i - f * a.n_kp);
-    const float* yf = a.y + f * 2 * a.n_kp + 2 * k;
-    const float px = kornia_denorm(yf[0], a.W);
-    const float py = kornia_denorm(yf[1], a.H);
+    double r[PPW][2], J[PPW][12], e[PPW];
+    int32_t stt[PPW];
+    int n[PPW];
+#pragma unroll
+    for (int h = 0; h < PPW; ++h) {
+      const long ib = (u * PPW + h) * 64;
+      n[h] = (int)(np - ib < 64 ? (np - ib > 0 ? np - ib : 0) : 64);
+      const long i = n[h] > 0 ? ib + (lane < n[h] ? lane : n[h] - 1) : np - 1;
+      const long f = i / a.n_kp;
+      const int k = (int)(i - f * a.n_kp);
+      const float* yf = a.y + f * 2 * a.n_kp + 2 * k;
+      const float px = kornia_denorm(yf[0], a.W);
+      const float py = kornia_denorm(yf[1], a.H);
+      // every output computed (no pointer selects: the arrays stay in registers)
+      proj_one(a.pose + f * 12, load3(a.corners + 3 * k), (double)px, (double)py, a.K, a.tcam, a.isig_proj, r[h],
+               J[h], &e[h], &stt[h]);
+    }
     int32_t* sst = reinterpret_cast<int32_t*>(st + 64 * 15);
-    proj_one(a.pose + f * 12, load3(a.corners + 3 * k), (double)px, (double)py, a.K, a.tcam, a.isig_proj,
-             st + lane * 2, a.j_proj ? st + 64 * 2 + lane * 12 : nullptr, a.err_proj ? st + 64 * 14 + lane : nullptr,
-             sst + lane);
-    wave_sync();
-    wave_flush(a.r_proj + i0 * 2, st, n, 2);
-    if (a.j_proj) wave_flush(a.j_proj + i0 * 12, st + 64 * 2, n, 12);
-    if (a.err_proj) wave_flush(a.err_proj + i0, st + 64 * 14, n, 1);
-    if (a.status && lane < n) a.status[i0 + lane] = sst[lane];
+#pragma unroll
+    for (int h = 0; h < PPW; ++h) {
+      if (n[h] <= 0) break;  // wave-uniform
+      const long i0 = (u * PPW + h) * 64;
+      if (h) wave_sync();  // the previous flush's LDS reads are done
+      st[lane * 2] = r[h][0];
+      st[lane * 2 + 1] = r[h][1];
+      if (a.j_proj) {
+#pragma unroll
+        for (int c = 0; c < 12; ++c) st[64 * 2 + lane * 12 + c] = J[h][c];
+      }
+      if (a.err_proj) st[64 * 14 + lane] = e[h];
+      sst[lane] = stt[h];
+      wave_sync();
+      wave_flush(a.r_proj + i0 * 2, st, n[h], 2);
+      if (a.j_proj) wave_flush(a.j_proj + i0 * 12, st + 64 * 2, n[h], 12);
+      if (a.err_proj) wave_flush(a.err_proj + i0, st + 64 * 14, n[h], 1);
+      if (a.status && lane < n[h]) a.status[i0 + lane] = sst[lane];
+    }
     return;
   }
   const long c0 = (u - wp) * 64;  // ConstantVelocityFactor (l, l+1)
@@ -792,7 +807,7 @@ int pa_trajectory_linearize(const pa_traj_args* a, void* stream) {
   PA_CHECK(a->r_proj && (a->L == 1 || (a->r_dyn && a->r_cv)), "null output pointer");
   PA_CHECK(a->vel_frame == PA_VEL_WORLD || a->vel_frame == PA_VEL_BODY, "vel_frame must be 'world' or 'body'.");
   const long np = (long)a->T * a->L * a->n_kp, nd = (long)a->T * (a->L - 1);
-  const long units = (np + 63) / 64 + (nd + 63) / 64;  // projection | constant-velocity, two per workgroup
+  const long units = (np + 64 * pa::trj::PPW - 1) / (64 * pa::trj::PPW) + (nd + 63) / 64;  // projection | const-vel, two per workgroup
   hipLaunchKernelGGL(pa::traj_all_kernel, dim3((unsigned)((nd + 63) / 64 + (units + 1) / 2)), dim3(128), 0,
                      (hipStream_t)stream, *a);
   PA_LAUNCH_CHECK();
