@@ -756,10 +756,10 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
 // Also measured: two launches (the projection kernel at 76 VGPRs) 16.1 + 8.9 us; the
 // dynamics launch on a forked side stream 42 us; s_setprio on the dynamics waves: no
 // change; a lane PAIR per factor (both lanes running the shared chain, the Jacobian
-// halves as one instruction stream) 18.3 us.  This form: 15.3 us (dynamics workgroups
-// alone 12.7, projection / constant-velocity alone 11.3 at 45 KB of LDS per workgroup;
-// the 35 KB layout adds a fourth workgroup per CU).  Three waves per SIMD does not fit
-// (the compiler keeps 200 VGPRs).
+// halves as one instruction stream) 18.3 us.  Two-wave dynamics workgroups: 15.3 us
+// (dynamics alone 12.7, projection / constant-velocity alone 11.3 at 45 KB of LDS per
+// workgroup; four workgroups per CU since); H0 / J0 moved to wave 1 (one barrier) and four
+// projection factors per lane: 14.7 us.  Three waves per SIMD does not fit (~220 VGPRs).
 __global__ __launch_bounds__(128, 2) void traj_all_kernel(pa_traj_args a) {
   __shared__ __attribute__((aligned(16))) double st[trj::STAGE];
   const long wd = ((long)a.T * (a.L - 1) + 63) / 64;
