@@ -8,7 +8,10 @@ int launch_conv3x3s2_x3(const ConvS2Args& a, hipStream_t s, const char** kname) 
   if (a.B <= 0) return PA_OK;
   if (a.Hout == 32 && a.Cin == 64) {
     if (kname) *kname = "conv3x3s2x3_l2";
-    return run_s2x<4, 16, 128, 2, 2, 64, 3, 1, true, true>(a, true, s);  // 2 patch buffers: 4-row tile
+    // 8 waves of 32 x 32 (210 VGPRs): 55.1 us against 60.9 for 4 waves of 32 x 64 (366 VGPRs, one
+    // wave per SIMD, variant 44); multi-tile workgroups spill here (85 / 77 us)
+    if (g_variant[6] == 44) return run_s2x<4, 16, 128, 2, 2, 64, 3, 1, true, true>(a, true, s);
+    return run_s2x<4, 16, 128, 2, 4, 64, 3, 1, true, true>(a, true, s);  // 2 patch buffers: 4-row tile
   }
   if (a.Hout == 16 && a.Cin == 128) {
     if (kname) *kname = "conv3x3s2x3_l3";

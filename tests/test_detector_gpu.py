@@ -243,6 +243,19 @@ def test_profile_reports_every_kernel():
     assert [n for n, _ in prof32][:2] == ["stem_conv7x7", "maxpool"]
 
 
+def test_fp16x3_stride2_variants_agree_bit_for_bit():
+    """fp16x3: the layer2 stride-2 entry's 8-wave tile (shipped) against the 4-wave one."""
+    m = model(0, precision="fp16x3")
+    x = torch.from_numpy(synth.synthetic_frames(4, 5)).cuda()
+    y0 = m(x)
+    try:
+        m.set_variants({6: 44})
+        y1 = m(x)
+    finally:
+        m.set_variants({})
+    assert torch.equal(y0, y1)
+
+
 @pytest.mark.parametrize("B", [1, 3, 64])
 def test_kernel_variants_agree_bit_for_bit(B):
     """The persistent kernels (layer1 weight-resident conv, stride-2 + downsample)
