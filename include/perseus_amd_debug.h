@@ -23,6 +23,12 @@ int pa_detector_debug_set_variant(pa_detector* d, int layer, int variant);
  * NULL turns it off. */
 int pa_detector_debug_set_trace(pa_detector* d, unsigned long long* trace_dev);
 
+/* Timing only: pa_trajectory_linearize with mode 1 = only the dynamics workgroups,
+ * 2 = only the projection / constant-velocity workgroups (the other outputs are left
+ * unwritten); mode 0 is pa_trajectory_linearize itself.  A non-NULL trace_dev (8 u64
+ * per wave, 2 waves per workgroup) receives s_memrealtime stamps at each wave's phases. */
+int pa_debug_trajectory_linearize(const pa_traj_args* args, int mode, unsigned long long* trace_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,6 +37,7 @@ class TrajArgs(C.Structure):
 # name -> (restype, argtypes)
 _SIGS = {
     "pa_trajectory_linearize": (C.c_int, [C.POINTER(TrajArgs), C.c_void_p]),
+    "pa_debug_trajectory_linearize": (C.c_int, [C.POINTER(TrajArgs), C.c_int, C.c_void_p, C.c_void_p]),
     "pa_last_error": (C.c_char_p, []),
     "pa_version": (C.c_char_p, []),
     "pa_detector_create": (C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -533,10 +533,28 @@ constexpr int UNIT = 64 * 22;  // projection / constant-velocity staging per wav
 static_assert(2 * UNIT <= STAGE, "unit staging");
 }  // namespace trj
 
-// the wave's n records of `per` doubles, staged at st[lane * per ..], -> dst[0 .. n * per)
-__device__ __forceinline__ void wave_flush(double* __restrict__ dst, const double* st, int n, int per) {
-  const int lane = threadIdx.x & 63, nd = n * per;
+// the wave's n records of PER doubles, staged at st[lane * PER ..], -> dst[0 .. n * PER).
+// A full wave (n = 64) to a 16-B aligned dst takes the unrolled path: the LDS reads of a
+// batch of 6 are issued before its stores (the rolled loop waited out one LDS round trip
+// per 1 KB store: ~2 us of a 36-double flush, tools/traj_exp.py --trace)
+template <int PER>
+__device__ __forceinline__ void wave_flush(double* __restrict__ dst, const double* st, int n) {
+  const int lane = threadIdx.x & 63, nd = n * PER;
   if (!dst) return;
+  if (n == 64 && ((uintptr_t)dst & 15) == 0) {
+    constexpr int N2 = 32 * PER, NI = (N2 + 63) / 64, BT = 6;
+#pragma unroll
+    for (int b = 0; b < NI; b += BT) {
+      double2 v[BT];
+#pragma unroll
+      for (int i = 0; i < BT; ++i)
+        if (b + i < NI && (b + i) * 64 + lane < N2) v[i] = reinterpret_cast<const double2*>(st)[(b + i) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < BT; ++i)
+        if (b + i < NI && (b + i) * 64 + lane < N2) reinterpret_cast<double2*>(dst)[(b + i) * 64 + lane] = v[i];
+    }
+    return;
+  }
   if (((uintptr_t)dst & 15) == 0) {
     for (int c = lane; c < nd / 2; c += 64)
       reinterpret_cast<double2*>(dst)[c] = reinterpret_cast<const double2*>(st)[c];
@@ -544,6 +562,12 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ dst, const doubl
   } else {
     for (int c = lane; c < nd; c += 64) dst[c] = st[c];
   }
+}
+
+// timing only (pa_debug_trajectory_linearize with a trace buffer): s_memrealtime (100 MHz)
+// per wave, 8 slots at trace[(workgroup * 2 + wave) * 8 + slot]
+__device__ __forceinline__ void traj_stamp(unsigned long long* ts, int slot) {
+  if (ts && (threadIdx.x & 63) == 0) ts[(blockIdx.x * 2 + (threadIdx.x >> 6)) * 8 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // wave-local LDS ordering: the staging of one wave is written and flushed by that wave only
@@ -570,7 +594,7 @@ __device__ __forceinline__ void stage6x3(double* J, bool has_top, const M3& top,
 //           dtw = dt A D and H0 = A Ad(inc^-1); writes J1, J2, J0
 // A goes 0 -> 1 through LDS (one barrier).  The products and their order are dyn_one's
 // (factors.py:54-142), so the values are the same; wave 0 holds only the chain and dlog.
-__device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, double* st) {
+__device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, double* st, unsigned long long* ts) {
   using namespace trj;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long nd = (long)a.T * (a.L - 1);
@@ -584,10 +608,15 @@ __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, 
   double sw[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) sw[i] = a.isig_dyn ? a.isig_dyn[i] : 1.0;
+  traj_stamp(ts, 0);
   const Pose T1 = load_pose(a.pose + f * 12);
   const V3 w = load3(a.angvel + f * 3);
   V3 vb = load3(a.vel + f * 3);
   if (world) vb = mtv(T1.R, vb);  // transformTo / unrotate (factors.py:100,134)
+  if (ts) {
+    asm volatile("" ::"v"(vb.x), "v"(T1.R.a[0]), "v"(w.x));  // the loads have landed
+    traj_stamp(ts, 1);
+  }
   const V3 xw = dt * w, xv = dt * vb;
   const Ang ax = ang(xw);  // |xi_w| for Expmap, ExpmapDerivative and Q
   const Pose inc = pose_exp(xw, xv, ax);  // Expmap (:104 / :136)
@@ -618,7 +647,9 @@ __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, 
         XAp[9 + i] = A.C.a[i];
       }
     }
+    traj_stamp(ts, 2);
     lds_barrier();  // A -> wave 1
+    traj_stamp(ts, 3);
     // r | J3 = dlog * I (:130) | err
     double* sr = st + W0 + lane * 6;
     double* s3 = st + W0 + 64 * 6 + lane * 36;
@@ -633,16 +664,23 @@ __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, 
       }
     }
     wave_sync();
-    wave_flush(a.r_dyn + j0 * 6, st + W0, n, 6);
-    if (a.j_dyn3) wave_flush(a.j_dyn3 + j0 * 36, st + W0 + 64 * 6, n, 36);
-    if (a.err_dyn) wave_flush(a.err_dyn + j0, st + W0 + 64 * 42, n, 1);
+    wave_flush<6>(a.r_dyn + j0 * 6, st + W0, n);
+    if (a.j_dyn3) wave_flush<36>(a.j_dyn3 + j0 * 36, st + W0 + 64 * 6, n);
+    if (a.err_dyn) wave_flush<1>(a.err_dyn + j0, st + W0 + 64 * 42, n);
+    traj_stamp(ts, 4);
+    if (ts) {
+      __builtin_amdgcn_s_waitcnt(0);
+      traj_stamp(ts, 7);
+    }
   } else {
     BL D{}, Ainc{};
     if (J) {
       D = BL{rot_dexp(xw, ax), compute_q(xw, xv, ax)};  // ExpmapDerivative(xi)
       Ainc = adjoint_bl(inverse(inc));
     }
+    traj_stamp(ts, 2);
     lds_barrier();  // A <- wave 0
+    traj_stamp(ts, 3);
     if (!J) return;
     BL A;
 #pragma unroll
@@ -665,19 +703,24 @@ __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, 
         stage6x3(s1 + lane * 36 + 18, false, H0.A, H0.A, sw);
       }
       wave_sync();
-      wave_flush(a.j_dyn0 + j0 * 36, s1, n, 36);
+      wave_flush<36>(a.j_dyn0 + j0 * 36, s1, n);
       wave_sync();
     }
     if (a.j_dyn1) {  // dtw[:, :3] (:117-118)
       if (lane < n) stage6x3(s1 + lane * 18, true, dtw.A, dtw.C, sw);
       wave_sync();
-      wave_flush(a.j_dyn1 + j0 * 18, s1, n, 18);
+      wave_flush<18>(a.j_dyn1 + j0 * 18, s1, n);
       wave_sync();
     }
     if (a.j_dyn2) {  // J2 = dtw[:, 3:] @ R1^T (world, :125) or dtw[:, 3:] (body, :128); dtw[:3, 3:] = 0
       if (lane < n) stage6x3(s1 + lane * 18, false, dtw.A, world ? mul(dtw.A, tr(T1.R)) : dtw.A, sw);
       wave_sync();
-      wave_flush(a.j_dyn2 + j0 * 18, s1, n, 18);
+      wave_flush<18>(a.j_dyn2 + j0 * 18, s1, n);
+    }
+    traj_stamp(ts, 4);
+    if (ts) {
+      __builtin_amdgcn_s_waitcnt(0);
+      traj_stamp(ts, 7);
     }
   }
 }
@@ -689,12 +732,13 @@ __device__ __forceinline__ void traj_dyn_block(const pa_traj_args& a, long blk, 
 namespace trj {
 constexpr int PPW = 4;  // projection factors per lane
 }
-__device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, double* st) {
+__device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, double* st, unsigned long long* ts) {
   using trj::PPW;
   const int lane = threadIdx.x & 63;
   const long F = (long)a.T * a.L;
   const long np = F * a.n_kp, nd = (long)a.T * (a.L - 1);
   const long wp = (np + 64 * PPW - 1) / (64 * PPW);
+  traj_stamp(ts, 0);
   if (u < wp) {  // KeypointProjectionFactor, factor i = f * K + k
     double r[PPW][2], J[PPW][12], e[PPW];
     int32_t stt[PPW];
@@ -713,6 +757,10 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
       proj_one(a.pose + f * 12, load3(a.corners + 3 * k), (double)px, (double)py, a.K, a.tcam, a.isig_proj, r[h],
                J[h], &e[h], &stt[h]);
     }
+    if (ts) {
+      asm volatile("" ::"v"(r[0][0]), "v"(r[PPW - 1][1]), "v"(J[PPW - 1][11]));  // compute done
+      traj_stamp(ts, 2);
+    }
     int32_t* sst = reinterpret_cast<int32_t*>(st + 64 * 15);
 #pragma unroll
     for (int h = 0; h < PPW; ++h) {
@@ -728,10 +776,15 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
       if (a.err_proj) st[64 * 14 + lane] = e[h];
       sst[lane] = stt[h];
       wave_sync();
-      wave_flush(a.r_proj + i0 * 2, st, n[h], 2);
-      if (a.j_proj) wave_flush(a.j_proj + i0 * 12, st + 64 * 2, n[h], 12);
-      if (a.err_proj) wave_flush(a.err_proj + i0, st + 64 * 14, n[h], 1);
+      wave_flush<2>(a.r_proj + i0 * 2, st, n[h]);
+      if (a.j_proj) wave_flush<12>(a.j_proj + i0 * 12, st + 64 * 2, n[h]);
+      if (a.err_proj) wave_flush<1>(a.err_proj + i0, st + 64 * 14, n[h]);
       if (a.status && lane < n[h]) a.status[i0 + lane] = sst[lane];
+    }
+    traj_stamp(ts, 4);
+    if (ts) {
+      __builtin_amdgcn_s_waitcnt(0);
+      traj_stamp(ts, 7);
     }
     return;
   }
@@ -743,10 +796,15 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
   cv_one(a.vel + f * 3, a.vel + (f + 1) * 3, a.isig_cv, st + lane * 3, a.j_cv0 ? st + 64 * 3 + lane * 9 : nullptr,
          a.j_cv1 ? st + 64 * 12 + lane * 9 : nullptr, a.err_cv ? st + 64 * 21 + lane : nullptr);
   wave_sync();
-  wave_flush(a.r_cv + c0 * 3, st, n, 3);
-  if (a.j_cv0) wave_flush(a.j_cv0 + c0 * 9, st + 64 * 3, n, 9);
-  if (a.j_cv1) wave_flush(a.j_cv1 + c0 * 9, st + 64 * 12, n, 9);
-  if (a.err_cv) wave_flush(a.err_cv + c0, st + 64 * 21, n, 1);
+  wave_flush<3>(a.r_cv + c0 * 3, st, n);
+  if (a.j_cv0) wave_flush<9>(a.j_cv0 + c0 * 9, st + 64 * 3, n);
+  if (a.j_cv1) wave_flush<9>(a.j_cv1 + c0 * 9, st + 64 * 12, n);
+  if (a.err_cv) wave_flush<1>(a.err_cv + c0, st + 64 * 21, n);
+  traj_stamp(ts, 4);
+  if (ts) {
+    __builtin_amdgcn_s_waitcnt(0);
+    traj_stamp(ts, 7);
+  }
 }
 
 // one launch, the dynamics workgroups dispatched first: they hold the longest per-lane
@@ -760,14 +818,19 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
 // (dynamics alone 12.7, projection / constant-velocity alone 11.3 at 45 KB of LDS per
 // workgroup; four workgroups per CU since); H0 / J0 moved to wave 1 (one barrier) and four
 // projection factors per lane: 14.7 us.  Three waves per SIMD does not fit (~220 VGPRs).
-__global__ __launch_bounds__(128, 2) void traj_all_kernel(pa_traj_args a) {
+// mode (pa_debug_trajectory_linearize, timing only): 1 = dynamics workgroups only,
+// 2 = projection / constant-velocity workgroups only
+__global__ __launch_bounds__(128, 2) void traj_all_kernel(pa_traj_args a, int mode, unsigned long long* ts) {
   __shared__ __attribute__((aligned(16))) double st[trj::STAGE];
   const long wd = ((long)a.T * (a.L - 1) + 63) / 64;
   if ((long)blockIdx.x < wd) {
-    traj_dyn_block(a, blockIdx.x, st);
+    if (mode == 2) return;
+    traj_dyn_block(a, blockIdx.x, st, ts);
+  } else if (mode == 1) {
+    return;
   } else {
     const int wv = threadIdx.x >> 6;
-    traj_unit_wave(a, 2 * ((long)blockIdx.x - wd) + wv, st + wv * trj::UNIT);
+    traj_unit_wave(a, 2 * ((long)blockIdx.x - wd) + wv, st + wv * trj::UNIT, ts);
   }
 }
 
@@ -799,7 +862,7 @@ int pa_cv_linearize(int n, const double* v1, const double* v2, const double* inv
   return PA_OK;
 }
 
-int pa_trajectory_linearize(const pa_traj_args* a, void* stream) {
+int pa_debug_trajectory_linearize(const pa_traj_args* a, int mode, unsigned long long* trace, void* stream) {
   PA_CHECK(a, "null args");
   PA_CHECK(a->T >= 0 && a->L >= 1 && a->n_kp >= 1, "T=%d L=%d n_kp=%d", a->T, a->L, a->n_kp);
   if (a->T == 0) return PA_OK;
@@ -809,9 +872,13 @@ int pa_trajectory_linearize(const pa_traj_args* a, void* stream) {
   const long np = (long)a->T * a->L * a->n_kp, nd = (long)a->T * (a->L - 1);
   const long units = (np + 64 * pa::trj::PPW - 1) / (64 * pa::trj::PPW) + (nd + 63) / 64;  // projection | const-vel, two per workgroup
   hipLaunchKernelGGL(pa::traj_all_kernel, dim3((unsigned)((nd + 63) / 64 + (units + 1) / 2)), dim3(128), 0,
-                     (hipStream_t)stream, *a);
+                     (hipStream_t)stream, *a, mode, trace);
   PA_LAUNCH_CHECK();
   return PA_OK;
+}
+
+int pa_trajectory_linearize(const pa_traj_args* a, void* stream) {
+  return pa_debug_trajectory_linearize(a, 0, nullptr, stream);
 }
 
 int pa_proj_linearize(int n, const double* tbody, const double* pb, const double* z, const double* k, int k_stride,
