@@ -402,8 +402,6 @@ static int run_patch(const ConvArgs& a, hipStream_t s) {
 // Stride-1 3x3 conv, Hin == Hout.  Tile configuration per feature-map size;
 // g_variant[layer] (the handle's pa_detector_debug_set_variant) selects alternatives
 // for A/B timing.
-int launch_conv3x3_c64w(const ConvArgs& a, hipStream_t s);  // conv_c64w.hip
-
 static const int k_shipped_variants[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 thread_local const int* g_variant = k_shipped_variants;
 thread_local unsigned long long* g_trace = nullptr;
@@ -439,11 +437,6 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
     if (l1 && c64) {
       if (kname) *kname = "conv3x3c64_l1";
       return launch_conv3x3_c64(a, g_variant[1] - 30, s);
-    }
-    if (l1 && (g_variant[1] == 70 || g_variant[1] == 71)) {  // 71: c64w on the non-residual convs only
-      if (kname) *kname = "conv3x3c64_l1";
-      if (g_variant[1] == 71 && (a.epi & EPI_RES)) return launch_conv3x3_c64d(a, 0, s);
-      return launch_conv3x3_c64w(a, s);
     }
     if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && g_variant[1] >= 60 && g_variant[1] <= 69) {
       if (kname) *kname = "conv3x3c64_l1";

@@ -438,44 +438,47 @@ __global__ __launch_bounds__(64) void cv_kernel(int n, const double* __restrict_
          err ? err + u : nullptr);
 }
 
-// One KeypointProjectionFactor.  K: 5 values; Tc: 12 values or null (identity);
-// outputs r 2, J 12 (col-major 2x6) or null, err / status or null.
-__device__ void proj_one(const double* __restrict__ Tb, V3 pb, double zx, double zy, const double* __restrict__ K,
-                         const double* __restrict__ Tcp, const double* __restrict__ isig, double* __restrict__ r_out,
-                         double* __restrict__ J, double* __restrict__ err, int32_t* __restrict__ status) {
-  const Pose T = load_pose(Tb);
-  const double fx = K[0], fy = K[1], sk = K[2], u0 = K[3], v0 = K[4];
+// One KeypointProjectionFactor on preloaded operands (T: body pose, C: camera pose, cal:
+// fx, fy, s, u0, v0, s0 / s1: whitening), branch-free: the cheirality case (pc.z <= 0)
+// is a select at the end, so the caller can interleave several factors' loads and
+// arithmetic (a branch per factor kept the traj kernel's four per-lane factors in
+// sequence, each waiting out its own loads).  Outputs r 2, J 12 (col-major 2x6), err,
+// status.
+struct Cam {
   Pose C;
+  double fx, fy, sk, u0, v0, s0, s1;
+};
+__device__ __forceinline__ Cam load_cam(const double* __restrict__ K, const double* __restrict__ Tcp,
+                                        const double* __restrict__ isig) {
+  Cam c;
   if (Tcp) {
-    C = load_pose(Tcp);
+    c.C = load_pose(Tcp);
   } else {
-    C.R = eye3();
-    C.t = v3(0, 0, 0);
+    c.C.R = eye3();
+    c.C.t = v3(0, 0, 0);
   }
+  c.fx = K[0];
+  c.fy = K[1];
+  c.sk = K[2];
+  c.u0 = K[3];
+  c.v0 = K[4];
+  c.s0 = isig ? isig[0] : 1.0;
+  c.s1 = isig ? isig[1] : 1.0;
+  return c;
+}
+__device__ __forceinline__ void proj_eval(const Pose& T, V3 pb, double zx, double zy, const Cam& cam, double (&r_out)[2],
+                                          double (&J)[12], double& err, int32_t& status) {
+  const Pose& C = cam.C;
+  const double fx = cam.fx, fy = cam.fy, sk = cam.sk, u0 = cam.u0, v0 = cam.v0, s0 = cam.s0, s1 = cam.s1;
   // transformFrom (factors.py:257): pw = R pb + t, d/dpose = [R skew(-pb), R]
   const V3 pw = mv(T.R, pb) + T.t;
   // PinholeCamera::project (:260-261): pc = Rc^T (pw - tc), cheirality pc.z <= 0
   const V3 pc = mtv(C.R, pw - C.t);
-  const double s0 = isig ? isig[0] : 1.0, s1 = isig ? isig[1] : 1.0;
-  if (!(pc.z > 0.0)) {
-    const double nan = __builtin_nan("");
-    r_out[0] = nan;
-    r_out[1] = nan;
-    if (J)
-      for (int k = 0; k < 12; ++k) J[k] = nan;
-    if (err) *err = nan;
-    if (status) *status = 1;
-    return;
-  }
+  const bool ok = pc.z > 0.0;
   const double iz = 1.0 / pc.z;
   const double x = pc.x * iz, y = pc.y * iz;
   const double u = fx * x + sk * y + u0, v = fy * y + v0;
   const double r0 = (u - zx) * s0, r1 = (v - zy) * s1;
-  r_out[0] = r0;
-  r_out[1] = r1;
-  if (err) *err = 0.5 * (r0 * r0 + r1 * r1);
-  if (status) *status = 0;
-  if (!J) return;
   // dproj_dpoint = Dcal * Dpn * Rc^T (2x3), Dcal = [[fx, s],[0, fy]], Dpn = 1/z [[1,0,-x],[0,1,-y]]
   double Dpn[2][3] = {{iz, 0.0, -x * iz}, {0.0, iz, -y * iz}};
   double Dp[2][3];
@@ -488,16 +491,39 @@ __device__ void proj_one(const double* __restrict__ Tb, V3 pb, double zx, double
     for (int c = 0; c < 3; ++c) Dw[rr][c] = Dp[rr][0] * C.R(c, 0) + Dp[rr][1] * C.R(c, 1) + Dp[rr][2] * C.R(c, 2);
   // dpc_dpose = [R skew(-pb), R]
   const M3 RS = mul(T.R, skew(-1.0 * pb));
+  const double nan = __builtin_nan("");
   for (int c = 0; c < 6; ++c) {
     double h[2];
     for (int rr = 0; rr < 2; ++rr) {
-      double s = 0.0;
-      for (int k = 0; k < 3; ++k) s += Dw[rr][k] * (c < 3 ? RS(k, c) : T.R(k, c - 3));
-      h[rr] = s;
+      double sacc = 0.0;
+      for (int k = 0; k < 3; ++k) sacc += Dw[rr][k] * (c < 3 ? RS(k, c) : T.R(k, c - 3));
+      h[rr] = sacc;
     }
-    J[c * 2] = h[0] * s0;  // H0 = dproj_dpoint @ dpc_dpose (:264), column-major
-    J[c * 2 + 1] = h[1] * s1;
+    J[c * 2] = ok ? h[0] * s0 : nan;  // H0 = dproj_dpoint @ dpc_dpose (:264), column-major
+    J[c * 2 + 1] = ok ? h[1] * s1 : nan;
   }
+  r_out[0] = ok ? r0 : nan;
+  r_out[1] = ok ? r1 : nan;
+  err = ok ? 0.5 * (r0 * r0 + r1 * r1) : nan;
+  status = ok ? 0 : 1;
+}
+
+// One KeypointProjectionFactor.  K: 5 values; Tc: 12 values or null (identity);
+// outputs r 2, J 12 (col-major 2x6) or null, err / status or null.
+__device__ void proj_one(const double* __restrict__ Tb, V3 pb, double zx, double zy, const double* __restrict__ K,
+                         const double* __restrict__ Tcp, const double* __restrict__ isig, double* __restrict__ r_out,
+                         double* __restrict__ J, double* __restrict__ err, int32_t* __restrict__ status) {
+  const Pose T = load_pose(Tb);
+  const Cam cam = load_cam(K, Tcp, isig);
+  double r[2], Jl[12], e;
+  int32_t st;
+  proj_eval(T, pb, zx, zy, cam, r, Jl, e, st);
+  r_out[0] = r[0];
+  r_out[1] = r[1];
+  if (err) *err = e;
+  if (status) *status = st;
+  if (J)
+    for (int k = 0; k < 12; ++k) J[k] = Jl[k];
 }
 
 __global__ __launch_bounds__(64) void proj_kernel(int n, const double* __restrict__ Tb, const double* __restrict__ pbp,
@@ -743,6 +769,12 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
     double r[PPW][2], J[PPW][12], e[PPW];
     int32_t stt[PPW];
     int n[PPW];
+    // every operand of the PPW factors is loaded before any is used (proj_eval is
+    // branch-free, so the loads of all PPW chains are in flight together)
+    const Cam cam = load_cam(a.K, a.tcam, a.isig_proj);
+    Pose T[PPW];
+    V3 pb[PPW];
+    float2 yv[PPW];
 #pragma unroll
     for (int h = 0; h < PPW; ++h) {
       const long ib = (u * PPW + h) * 64;
@@ -751,11 +783,15 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
       const long f = i / a.n_kp;
       const int k = (int)(i - f * a.n_kp);
       const float* yf = a.y + f * 2 * a.n_kp + 2 * k;
-      const float px = kornia_denorm(yf[0], a.W);
-      const float py = kornia_denorm(yf[1], a.H);
-      // every output computed (no pointer selects: the arrays stay in registers)
-      proj_one(a.pose + f * 12, load3(a.corners + 3 * k), (double)px, (double)py, a.K, a.tcam, a.isig_proj, r[h],
-               J[h], &e[h], &stt[h]);
+      yv[h] = float2{yf[0], yf[1]};
+      T[h] = load_pose(a.pose + f * 12);
+      pb[h] = load3(a.corners + 3 * k);
+    }
+#pragma unroll
+    for (int h = 0; h < PPW; ++h) {
+      const float px = kornia_denorm(yv[h].x, a.W);
+      const float py = kornia_denorm(yv[h].y, a.H);
+      proj_eval(T[h], pb[h], (double)px, (double)py, cam, r[h], J[h], e[h], stt[h]);
     }
     if (ts) {
       asm volatile("" ::"v"(r[0][0]), "v"(r[PPW - 1][1]), "v"(J[PPW - 1][11]));  // compute done
