@@ -260,8 +260,8 @@ def test_fp16x3_stride2_variants_agree_bit_for_bit():
 def test_kernel_variants_agree_bit_for_bit(B):
     """The persistent kernels (layer1 weight-resident conv, stride-2 + downsample)
     and the one-tile-per-workgroup kernels they replace accumulate in the same order:
-    identical outputs, at batches below and above one tile per CU.  (Stem variant 10
-    is the same stem kernel at a different band height.)"""
+    identical outputs, at batches below and above one tile per CU.  (Stem variants 10
+    and 16 are version 3 of the stem at two band heights.)"""
     m = model(0)
     x = torch.from_numpy(synth.synthetic_frames(2, B)).cuda()
     y0 = m(x)
@@ -273,6 +273,7 @@ def test_kernel_variants_agree_bit_for_bit(B):
         ((6, 11),),  # stride-2 entries: one tile per workgroup (layer2: the round-2a 8x16 kernel)
         ((6, 26),),  # multi-tile workgroups: layer2 4 waves of 32x64; layer3 as shipped
         ((6, 27),),  # layer2 prefetch distance 3; layer3 two 4x16 tiles per workgroup
+        ((0, 16),),  # stem: version 3 (every wave convolves and moves rows) vs the shipped role split
     )
     for vs in sets:
         try:
