@@ -280,10 +280,19 @@ __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__
 // version 3 every wave did both halves and the SIMD partners alternated roles; the MFMA
 // pipe was busy about half of the launch.  Accumulation order (bias, then kh = 0..6) and
 // every rounding step are version 3's, so the pooled map is bit-identical.
-template <int PBT, int D, bool PRE = false>
+// DBG = 4 (timing only): s_memrealtime stamps, 64 per workgroup: slot j = wave 0 (convolving)
+// at pair j's barrier, 20 + j = wave 4 (moving) at pair j's barrier, 40 + j = wave 0 past it,
+// 60 = start, 61 = prologue barrier passed, 62 = wave 0 done, 63 = wave 4 done
+template <int PBT, int D, bool PRE = false, int DBG = 0>
 __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ x, int B, int Cin,
                                                       const _Float16* __restrict__ w, const float* __restrict__ bias,
-                                                      _Float16* __restrict__ out, RgbdSrc src) {
+                                                      _Float16* __restrict__ out, RgbdSrc src,
+                                                      unsigned long long* trace) {
+  auto stamp = [&](int slot) __attribute__((always_inline)) {
+    if constexpr (DBG == 4) {
+      if ((threadIdx.x & 63) == 0) trace[(blockIdx.y * gridDim.x + blockIdx.x) * 64 + slot] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
   using namespace stem;
   static_assert(RING >= 9 + 4 && D >= 2 && D <= 4, "ring / prefetch depth");
   constexpr int WSTAGE = RING * ROWB + 2 * CROWB + 64 * 4;
@@ -301,6 +310,7 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
   const int mt = tid & 255;  // thread index within the role
   const float* xn = x + (size_t)n * Cin * 256 * 256;
   const int hbase = 4 * p0 - 7;
+  if (wid == 0) stamp(60);
 
   // movers: thread mt takes pixels 4 lcg .. 4 lcg + 3 (all 4 channels) of row lr of a
   // 4-row group
@@ -392,6 +402,7 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
   else
     xwait_vm<0>();
   lds_barrier();
+  if (wid == 0) stamp(61);
 
   constexpr int TN = 4;
   if (!mover) {
@@ -405,49 +416,53 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
       constexpr int j = decltype(jc)::value;
       const int r0 = 2 * p0 - 2 + 2 * j;  // pair j: conv rows r0 = 2p, r0 + 1 (p = p0 - 1 + j)
       const int hs = 4 * p0 - 7 + 4 * j;
-      f32x4 acc[2][2][TN];  // [row t][column tile c][tn]
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int b = 0; b < TN; ++b) acc[t][c][b] = *reinterpret_cast<const f32x4*>(bl + b * 16 + q * 4);
-#pragma unroll
-      for (int kh = 0; kh < 7; ++kh) {
-        su32x4 fb[2][2];
+      // column tile c = 0's epilogue (V write) is placed after c = 1's MFMAs are issued, so
+      // its VALU work fills the MFMA pipe's shadow instead of following it
+      f32x4 acc[2][2][TN];  // [column tile c][row t][tn]
+      auto conv_tile = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int slot = (hs + 2 * t + kh + 64) & (RING - 1);
-            fb[t][c] = *reinterpret_cast<const su32x4*>(ring + slot * ROWB + (2 * (wid * 32 + c * 16 + r16)) * 8 + q * 16);
-          }
+          for (int b = 0; b < TN; ++b) acc[c][t][b] = *reinterpret_cast<const f32x4*>(bl + b * 16 + q * 4);
+        // the 9 input rows of this pair (row t + kh for conv row t, tap row kh), each read
+        // once and four taps' MFMAs (two tap rows) ahead of its first use
+        su32x4 fr[9];
+        auto rd = [&](int r) __attribute__((always_inline)) {
+          const int slot = (hs + r + 64) & (RING - 1);
+          fr[r] = *reinterpret_cast<const su32x4*>(ring + slot * ROWB + (2 * (wid * 32 + c * 16 + r16)) * 8 + q * 16);
+        };
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int r = 0; r < 4; ++r) rd(r);
 #pragma unroll
-          for (int c = 0; c < 2; ++c)
+        for (int kh = 0; kh < 7; ++kh) {
+          if (kh + 4 <= 8) rd(kh + 4);
+          __builtin_amdgcn_sched_barrier(0);  // keep each read two tap rows ahead (the scheduler sank them)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
-              acc[t][c][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, wf[kh][tn]),
-                                                                     __builtin_bit_cast(half8, fb[t][c]), acc[t][c][tn], 0,
-                                                                     0, 0);
-      }
-      // rows above the image (only the whole pair r0 = -2, -1) are 0 = max-pool's -inf
-      // padding, since every window keeps >= 1 real post-ReLU value
-      const half4 z4 = half4{0, 0, 0, 0};
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
+              acc[c][t][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, wf[kh][tn]),
+                                                                     __builtin_bit_cast(half8, fr[kh + 2 * t]), acc[c][t][tn],
+                                                                     0, 0, 0);
+        }
+      };
+      // rows above the image (only the whole pair r0 = -2, -1 of the first band) are 0 =
+      // max-pool's -inf padding, since every window keeps >= 1 real post-ReLU value
+      auto epi_tile = [&](int c) __attribute__((always_inline)) {
+        const half4 z4 = half4{0, 0, 0, 0};
         half4 v0[TN], v1[TN];
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            v0[tn][e] = (_Float16)acc[0][c][tn][e];
-            v1[tn][e] = (_Float16)acc[1][c][tn][e];
+            v0[tn][e] = (_Float16)acc[c][0][tn][e];
+            v1[tn][e] = (_Float16)acc[c][1][tn][e];
           }
           v0[tn] = __builtin_elementwise_max(v0[tn], z4);
           v1[tn] = __builtin_elementwise_max(v1[tn], z4);
-          if (r0 < 0) v1[tn] = z4;
+          if constexpr (j == 0) {
+            if (r0 < 0) v1[tn] = z4;
+          }
         }
         if constexpr (j >= 1) {
           char* vw = vring + (j & 1) * CROWB;
@@ -461,9 +476,16 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
         }
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) prev[c][tn] = v1[tn];
-      }
+      };
+      conv_tile(0);
+      conv_tile(1);
+      epi_tile(0);
+      epi_tile(1);
+      if (wid == 0) stamp(j);
       lds_barrier();
+      if (wid == 0) stamp(40 + j);
     });
+    if (wid == 0) stamp(62);
   } else {
     stem_for<0, PBT + 2>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
@@ -483,16 +505,22 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
         }
       }
       if constexpr (j < PBT) store_rows(hs + 9, pf[(j + 1) % D]);  // pair j + 1's new rows
+      if (wid == 4 && j <= PBT) stamp(20 + j);
       if constexpr (j <= PBT) lds_barrier();
     });
+    if constexpr (DBG == 4) {
+      __builtin_amdgcn_s_waitcnt(0);
+      if (wid == 4) stamp(63);
+    }
   }
 }
 
-template <int PBT, int D, bool PRE = false>
+template <int PBT, int D, bool PRE = false, int DBG = 0>
 static int run_stem4(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out, hipStream_t s,
-                     RgbdSrc src = RgbdSrc{}) {
+                     RgbdSrc src = RgbdSrc{}, unsigned long long* trace = nullptr) {
   PA_CHECK((size_t)B * 64 * 64 * 64 * 2 < 0x7fffffffu, "stem: output over 2 GB");
-  hipLaunchKernelGGL((stem_role_fp16<PBT, D, PRE>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out, src);
+  hipLaunchKernelGGL((stem_role_fp16<PBT, D, PRE, DBG>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out,
+                     src, trace);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -533,10 +561,14 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
       if (g_trace) return run_stem3<16, 2, true, 4>(x, B, Cin, w, bias, out, s, g_trace);  // timestamps
       break;
     case 16: return run_stem3<16, 2, true>(x, B, Cin, w, bias, out, s);  // version 3 (shipped until round 2)
+    case 24:
+      if (g_trace) return run_stem4<16, 2, false, 4>(x, B, Cin, w, bias, out, s, RgbdSrc{}, g_trace);  // timestamps
+      break;
     // shipped: version 4, the role split (29.3 vs 31.8 us per B = 64 launch, bit-identical;
     // prefetch depth 3 / 4 measured 29.7 / 30.4 us)
-    default: return run_stem4<16, 2>(x, B, Cin, w, bias, out, s);
+    default: break;
   }
+  return run_stem4<16, 2>(x, B, Cin, w, bias, out, s);  // also variants 14 / 24 without a trace buffer
 }
 
 }  // namespace pa
