@@ -282,7 +282,8 @@ __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__
 // every rounding step are version 3's, so the pooled map is bit-identical.
 // DBG = 4 (timing only): s_memrealtime stamps, 64 per workgroup: slot j = wave 0 (convolving)
 // at pair j's barrier, 20 + j = wave 4 (moving) at pair j's barrier, 40 + j = wave 0 past it,
-// 60 = start, 61 = prologue barrier passed, 62 = wave 0 done, 63 = wave 4 done
+// 60 = start, 61 = prologue barrier passed, 62 = wave 0 done, 63 = wave 4 done; 58 / 59 =
+// s_memtime (shader clock) at wave 0's start / end
 template <int PBT, int D, bool PRE = false, int DBG = 0>
 __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ x, int B, int Cin,
                                                       const _Float16* __restrict__ w, const float* __restrict__ bias,
@@ -311,6 +312,9 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
   const float* xn = x + (size_t)n * Cin * 256 * 256;
   const int hbase = 4 * p0 - 7;
   if (wid == 0) stamp(60);
+  if constexpr (DBG == 4) {  // shader-clock counter beside the 100 MHz one (slot 58 / 59: start / wave 0 done)
+    if (tid == 0) trace[(blockIdx.y * gridDim.x + blockIdx.x) * 64 + 58] = __builtin_amdgcn_s_memtime();
+  }
 
   // movers: thread mt takes pixels 4 lcg .. 4 lcg + 3 (all 4 channels) of row lr of a
   // 4-row group
@@ -436,7 +440,9 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
 #pragma unroll
         for (int kh = 0; kh < 7; ++kh) {
           if (kh + 4 <= 8) rd(kh + 4);
-          __builtin_amdgcn_sched_barrier(0);  // keep each read two tap rows ahead (the scheduler sank them)
+          // keep each read two tap rows ahead (the scheduler sank them); VALU / SALU / MFMA may
+          // still cross, so the first column tile's epilogue can fill the second tile's MFMA shadow
+          __builtin_amdgcn_sched_barrier(0x000E);
 #pragma unroll
           for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -448,6 +454,10 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
       };
       // rows above the image (only the whole pair r0 = -2, -1 of the first band) are 0 =
       // max-pool's -inf padding, since every window keeps >= 1 real post-ReLU value
+      // ReLU commutes with max: relu(max(a, b, c)) = max(a, b, c, 0), so the V row is
+      // max(prev, v0, max(v1, 0)) on the raw fp16 conv values, and prev (row 2p + 1) is kept
+      // raw as well -- the same fp16 values as ReLU-then-max, one packed max fewer per pair of
+      // channels
       auto epi_tile = [&](int c) __attribute__((always_inline)) {
         const half4 z4 = half4{0, 0, 0, 0};
         half4 v0[TN], v1[TN];
@@ -458,8 +468,6 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
             v0[tn][e] = (_Float16)acc[c][0][tn][e];
             v1[tn][e] = (_Float16)acc[c][1][tn][e];
           }
-          v0[tn] = __builtin_elementwise_max(v0[tn], z4);
-          v1[tn] = __builtin_elementwise_max(v1[tn], z4);
           if constexpr (j == 0) {
             if (r0 < 0) v1[tn] = z4;
           }
@@ -469,7 +477,8 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
           const int wo = wid * 32 + c * 16 + r16;
 #pragma unroll
           for (int tn = 0; tn < TN; ++tn) {
-            const half4 vv = __builtin_elementwise_max(prev[c][tn], __builtin_elementwise_max(v0[tn], v1[tn]));
+            const half4 vv = __builtin_elementwise_max(__builtin_elementwise_max(prev[c][tn], v0[tn]),
+                                                       __builtin_elementwise_max(v1[tn], z4));
             const int ch = tn * 16 + q * 4;
             *reinterpret_cast<half4*>(vw + crow_swz(wo, ch >> 3) + (ch & 7) * 2) = vv;
           }
@@ -486,10 +495,17 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
       if (wid == 0) stamp(40 + j);
     });
     if (wid == 0) stamp(62);
+    if constexpr (DBG == 4) {
+      if (tid == 0) trace[(blockIdx.y * gridDim.x + blockIdx.x) * 64 + 59] = __builtin_amdgcn_s_memtime();
+    }
   } else {
     stem_for<0, PBT + 2>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       const int hs = 4 * p0 - 7 + 4 * j;
+      if constexpr (DBG == 5) {  // timing only: movers idle (barriers only), wrong results
+        if constexpr (j <= PBT) lds_barrier();
+        return;
+      }
       // the rows of pair j + D (new rows hs + 9 + 4 (D - 1) ..) into pf[j % D]
       if constexpr (j + D <= PBT) load_rows(hs + 9 + 4 * (D - 1), pf[j % D]);
       if constexpr (j >= 2) {  // pooled row p0 + j - 2 from V(j - 1)
@@ -564,6 +580,7 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     case 24:
       if (g_trace) return run_stem4<16, 2, false, 4>(x, B, Cin, w, bias, out, s, RgbdSrc{}, g_trace);  // timestamps
       break;
+    case 26: return run_stem4<16, 2, false, 5>(x, B, Cin, w, bias, out, s);  // timing only: idle movers
     // shipped: version 4, the role split (29.3 vs 31.8 us per B = 64 launch, bit-identical;
     // prefetch depth 3 / 4 measured 29.7 / 30.4 us)
     default: break;

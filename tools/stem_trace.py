@@ -40,7 +40,9 @@ def main():
         hold = t[:, 40 + j] - t[:, j]  # wave 0 waiting at the barrier
         rows.append({"pair": j, "mfma_wave": med(w0), "mover_wave": med(w4), "wave0_barrier_wait": med(hold)})
         prev = t[:, 40 + j]
-    out = {"prologue": med(t[:, 61] - t[:, 60]), "start_skew": med(t[:, 60] - t0),
+    raw = buf[:256 * 64].cpu().numpy().reshape(256, 64).astype(np.float64)
+    clk = (raw[:, 59] - raw[:, 58]) / ((raw[:, 62] - raw[:, 60]) / 100.0)  # s_memtime ticks per us
+    out = {"shader_clock_ghz": round(float(np.median(clk)) / 1e3, 3), "prologue": med(t[:, 61] - t[:, 60]), "start_skew": med(t[:, 60] - t0),
            "wave0_done": med(t[:, 62] - t0), "wave4_done": med(t[:, 63] - t0), "pairs": rows}
     print(json.dumps(out))
 
