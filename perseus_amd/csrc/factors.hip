@@ -596,8 +596,11 @@ __device__ __forceinline__ void traj_stamp(unsigned long long* ts, int slot) {
   if (ts && (threadIdx.x & 63) == 0) ts[(blockIdx.x * 2 + (threadIdx.x >> 6)) * 8 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
-// wave-local LDS ordering: the staging of one wave is written and flushed by that wave only
-__device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// wave-local LDS ordering: the staging of one wave is written and flushed by that wave only,
+// and one wave's LDS instructions execute in issue order, so a compiler barrier is enough
+// (it was an lgkmcnt(0) wait: every stage -> flush -> restage round then drained the LDS
+// queue before the next round could be issued)
+__device__ __forceinline__ void wave_sync() { asm volatile("" ::: "memory"); }
 
 // 6 x 3 column-major block of a Jacobian: rows 0..2 from `top` (zero if !has_top), rows
 // 3..5 from `bot`, row-scaled by sw (references, not pointers: an address-taken M3 lives
