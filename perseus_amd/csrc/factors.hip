@@ -559,6 +559,8 @@ constexpr int UNIT = 64 * 22;  // projection / constant-velocity staging per wav
 static_assert(2 * UNIT <= STAGE, "unit staging");
 }  // namespace trj
 
+typedef unsigned fu32x4 __attribute__((ext_vector_type(4)));
+
 // the wave's n records of PER doubles, staged at st[lane * PER ..], -> dst[0 .. n * PER).
 // A full wave (n = 64) to a 16-B aligned dst takes the unrolled path: the LDS reads of a
 // batch of 6 are issued before its stores (the rolled loop waited out one LDS round trip
@@ -568,7 +570,11 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ dst, const doubl
   const int lane = threadIdx.x & 63, nd = n * PER;
   if (!dst) return;
   if (n == 64 && ((uintptr_t)dst & 15) == 0) {
+    // write-through (sc1) buffer stores, as the conv epilogues: the 54 MB of factor outputs
+    // otherwise sit dirty in the XCDs' L2s and the end-of-kernel release writes them back
+    // after the last wave
     constexpr int N2 = 32 * PER, NI = (N2 + 63) / 64, BT = 6;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int b = 0; b < NI; b += BT) {
       double2 v[BT];
@@ -577,7 +583,8 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ dst, const doubl
         if (b + i < NI && (b + i) * 64 + lane < N2) v[i] = reinterpret_cast<const double2*>(st)[(b + i) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < BT; ++i)
-        if (b + i < NI && (b + i) * 64 + lane < N2) reinterpret_cast<double2*>(dst)[(b + i) * 64 + lane] = v[i];
+        if (b + i < NI && (b + i) * 64 + lane < N2)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fu32x4, v[i]), rs, ((b + i) * 64 + lane) * 16, 0, 16);
     }
     return;
   }
