@@ -61,6 +61,25 @@ def _includes(path, seen=None):
     return seen
 
 
+STAMP = os.path.join(OBJDIR, "flags.stamp")
+
+
+def _flags_digest() -> str:
+    """Compilers, flags and arch the objects are built with: a change invalidates every
+    object (mtimes alone would link stale objects built with the old flags)."""
+    import hashlib
+
+    return hashlib.sha256(repr((HIPCC, FLAGS, ARCH, CXX, HOST_FLAGS)).encode()).hexdigest()
+
+
+def _stamp_ok() -> bool:
+    try:
+        with open(STAMP) as fh:
+            return fh.read().strip() == _flags_digest()
+    except OSError:
+        return False
+
+
 def _obj(src: str) -> str:
     return os.path.join(OBJDIR, os.path.splitext(os.path.basename(src))[0] + ".o")
 
@@ -74,7 +93,7 @@ def _stale(src: str) -> bool:
 
 
 def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not _stamp_ok():
         return False
     t = os.path.getmtime(LIB)
     return all(os.path.getmtime(p) <= t for p in _deps())
@@ -98,6 +117,10 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return LIB
     srcs = sources()
+    if not _stamp_ok():
+        force = True
+        if os.path.exists(STAMP):
+            os.remove(STAMP)
     todo = [s for s in srcs if force or _stale(s)]
     # the fully unrolled conv kernels take minutes: start the slowest (largest) first
     todo.sort(key=lambda p: -os.path.getsize(p) - sum(os.path.getsize(h) for h in _includes(p)))
@@ -111,6 +134,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB)
+    with open(STAMP, "w") as fh:
+        fh.write(_flags_digest() + "\n")
     if verbose:
         print(f"built {LIB} ({len(todo)} of {len(srcs)} objects recompiled)")
     return LIB

@@ -653,7 +653,8 @@ void pa_detector_destroy(pa_detector* d) {
 
 int pa_detector_reserve(pa_detector* d, int max_batch) {
   PA_CHECK(d && max_batch >= 0, "bad arguments");
-  return pa::ensure_ws(d, max_batch);
+  // forward / forward_rgbd never use more than one chunk's workspace
+  return pa::ensure_ws(d, max_batch < pa::kChunk ? max_batch : pa::kChunk);
 }
 
 int pa_detector_set_precision(pa_detector* d, int precision) {
@@ -664,7 +665,7 @@ int pa_detector_set_precision(pa_detector* d, int precision) {
     // keep the same batch capacity for the new element size
     const size_t old = d->ws_bytes;
     int bcap = 0;
-    while (bcap < (1 << 20) && pa::ws_need(bcap + 1, d->prec) <= old) ++bcap;
+    while (bcap < pa::kChunk && pa::ws_need(bcap + 1, d->prec) <= old) ++bcap;
     d->prec = precision;
     if (bcap > 0) return pa::ensure_ws(d, bcap);
   }
@@ -677,6 +678,8 @@ int pa_detector_forward(pa_detector* d, const float* x_dev, int B, float* y_dev,
 
 int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream, float* ms_out,
                         const char** names_out, int max_n) {
+  // one chunk's launch sequence: a larger batch would repeat the marks per chunk
+  PA_CHECK(B <= pa::kChunk, "profile: batch %d above the %d-frame chunk (profile one chunk)", B, pa::kChunk);
   pa::Prof p;
   p.s = (hipStream_t)stream;
   int rc = pa::forward(d, x_dev, B, y_dev, p.s, &p);
@@ -700,6 +703,7 @@ int pa_detector_profile(pa_detector* d, const float* x_dev, int B, float* y_dev,
 int pa_detector_time_launch(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream, int index,
                             int reps, float* avg_ms_out, const char** name_out) {
   PA_CHECK(index >= 0 && reps >= 1, "index %d reps %d", index, reps);
+  PA_CHECK(B <= pa::kChunk, "time_launch: batch %d above the %d-frame chunk (time one chunk)", B, pa::kChunk);
   pa::Prof p;
   p.s = (hipStream_t)stream;
   p.target = index;

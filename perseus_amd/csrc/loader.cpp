@@ -20,7 +20,10 @@
 #include <cstdint>
 #include <cstring>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -458,34 +461,59 @@ int load_item(const char* img_path, const char* depth_path, const char* seg_path
   return PA_OK;
 }
 
+// Every extern "C" entry point runs its body through `guarded`: a C++ exception
+// (bad_alloc from a header-sized buffer, system_error from thread creation) must not
+// cross the C ABI / ctypes boundary, where it would std::terminate the caller.
+template <class F>
+int guarded(const char* where, F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    ::pa::set_error("%s: out of host memory", where);
+    return PA_ENOMEM;
+  } catch (const std::exception& e) {
+    ::pa::set_error("%s: %s", where, e.what());
+    return PA_EINVAL;
+  } catch (...) {
+    ::pa::set_error("%s: unknown C++ exception", where);
+    return PA_EINVAL;
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
 int pa_png_info(const uint8_t* buf, size_t n, int* h, int* w, int* channels) {
-  Png p;
-  const int r = png_parse(buf, n, p, false);
-  if (r) return r;
-  if (h) *h = p.h;
-  if (w) *w = p.w;
-  if (channels) *channels = png_channels(p.ctype);
-  return PA_OK;
+  return guarded("pa_png_info", [&]() {
+    Png p;
+    const int r = png_parse(buf, n, p, false);
+    if (r) return r;
+    if (h) *h = p.h;
+    if (w) *w = p.w;
+    if (channels) *channels = png_channels(p.ctype);
+    return (int)PA_OK;
+  });
 }
 
 int pa_png_decode(const uint8_t* buf, size_t n, int rgb, uint8_t* out, size_t cap) {
-  return png_decode(buf, n, rgb, out, cap);
+  return guarded("pa_png_decode", [&]() { return png_decode(buf, n, rgb, out, cap); });
 }
 
 int pa_tiff_info(const uint8_t* buf, size_t n, int* h, int* w) {
-  Tif t;
-  const int r = tif_parse(buf, n, t);
-  if (r) return r;
-  if (h) *h = t.h;
-  if (w) *w = t.w;
-  return PA_OK;
+  return guarded("pa_tiff_info", [&]() {
+    Tif t;
+    const int r = tif_parse(buf, n, t);
+    if (r) return r;
+    if (h) *h = t.h;
+    if (w) *w = t.w;
+    return (int)PA_OK;
+  });
 }
 
-int pa_tiff_decode_f32(const uint8_t* buf, size_t n, float* out, size_t cap) { return tif_decode(buf, n, out, cap); }
+int pa_tiff_decode_f32(const uint8_t* buf, size_t n, float* out, size_t cap) {
+  return guarded("pa_tiff_decode_f32", [&]() { return tif_decode(buf, n, out, cap); });
+}
 
 int pa_load_keypoint_items(const char* const* image_paths, const char* const* depth_paths,
                            const char* const* seg_paths, const int32_t* asset_ids, int B, int h, int w,
@@ -505,25 +533,43 @@ int pa_load_keypoint_items(const char* const* image_paths, const char* const* de
   std::atomic<int> failed{0};
   std::mutex mu;
   std::string msg;
+  int first_rc = PA_OK;
   auto work = [&]() {
     std::vector<uint8_t> file, px;
     for (int i; !failed.load(std::memory_order_relaxed) && (i = next.fetch_add(1)) < B;) {
-      const int r = load_item(image_paths ? image_paths[i] : nullptr, depth_paths ? depth_paths[i] : nullptr,
-                              seg_paths ? seg_paths[i] : nullptr, asset_ids ? asset_ids[i] : 0, h, w,
-                              image ? image + (size_t)i * 3 * np : nullptr, depth ? depth + (size_t)i * np : nullptr,
-                              seg ? seg + (size_t)i * np : nullptr, file, px);
+      // pa_last_error is thread-local: the item's message is taken on the thread that failed
+      const int r = guarded("pa_load_keypoint_items", [&]() {
+        return load_item(image_paths ? image_paths[i] : nullptr, depth_paths ? depth_paths[i] : nullptr,
+                         seg_paths ? seg_paths[i] : nullptr, asset_ids ? asset_ids[i] : 0, h, w,
+                         image ? image + (size_t)i * 3 * np : nullptr, depth ? depth + (size_t)i * np : nullptr,
+                         seg ? seg + (size_t)i * np : nullptr, file, px);
+      });
       if (r) {
         std::lock_guard<std::mutex> g(mu);
-        if (!failed.exchange(1)) msg = std::string("item ") + std::to_string(i) + ": " + pa_last_error();
+        if (!failed.exchange(1)) {
+          msg = std::string("item ") + std::to_string(i) + ": " + pa_last_error();
+          first_rc = r;
+        }
       }
     }
   };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < n_threads; ++t) pool.emplace_back(work);
-  work();
-  for (auto& t : pool) t.join();
-  LD_CHECK(!failed.load(), "%s", msg.c_str());
-  return PA_OK;
+  return guarded("pa_load_keypoint_items", [&]() {
+    std::vector<std::thread> pool;
+    for (int t = 1; t < n_threads; ++t) {
+      try {
+        pool.emplace_back(work);
+      } catch (const std::system_error&) {
+        break;  // fewer threads: the calling thread and those already started finish the batch
+      }
+    }
+    work();
+    for (auto& t : pool) t.join();
+    if (failed.load()) {
+      ::pa::set_error("%s", msg.c_str());
+      return first_rc;
+    }
+    return (int)PA_OK;
+  });
 }
 
 }  // extern "C"

@@ -7,6 +7,13 @@ TIFF decoders, one call per batch over a pool of host threads) instead of PIL + 
 DataLoader worker processes.  `load_batch` returns a whole batch stacked (optionally in
 pinned memory, ready for an async copy to the GPU).
 
+One recorded deviation: `depth_image` is always f32.  tifffile returns the page's native
+dtype (data.py:79-80), so for the float32 depth TIFFs the reference's datagen writes
+(generate_and_label_keypoints.py:93) the items are identical; an integer (e.g. uint16)
+depth TIFF would come back as an integer tensor there and as the same values in f32 here.
+How tifffile itself decodes float TIFFs with predictor 2 is not pinned by any fixture
+(parity unpinned; tests/test_loader.py pins the stored samples instead).
+
 The HDF5 index (data.py:46-66: attrs W / H and, per split, weights, pixel_coordinates,
 asset_ids and the three file-name arrays) is read with h5py when it is importable; this
 image has no h5py, so `from_index` takes the same arrays directly.

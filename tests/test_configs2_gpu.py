@@ -87,17 +87,29 @@ def _free_port():
 
 
 def test_gather_keypoints_over_rccl_world_size_1():
-    """shard.gather_keypoints' nccl branch (count exchange + all_gather_into_tensor) on
-    device tensors; world size 1 is the most one GPU can host, so the single-rank
-    short-circuit is bypassed with force=True."""
+    """shard.gather_keypoints' nccl branch on device tensors: with static counts exactly
+    one all_gather_into_tensor (RCCL), without them a count exchange first; world size 1
+    is the most one GPU can host, so the single-rank short-circuit is bypassed with
+    force=True."""
     assert not dist.is_initialized()
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     try:
         assert dist.get_backend() == "nccl"
         y = torch.randn(37, 16, device="cuda")
-        g = shard.gather_keypoints(y, force=True)
-        assert g.device.type == "cuda" and torch.equal(g, y)
+        calls = []
+        orig = {n: getattr(dist, n) for n in ("all_gather", "all_gather_into_tensor")}
+        for n, f in orig.items():
+            setattr(dist, n, lambda *a, _f=f, _n=n, **k: (calls.append(_n), _f(*a, **k))[1])
+        try:
+            g = shard.gather_keypoints(y, force=True, counts=shard.shard_counts(37, 1))
+            assert calls == ["all_gather_into_tensor"], calls
+            g2 = shard.gather_keypoints(y, force=True)
+            assert calls == ["all_gather_into_tensor", "all_gather", "all_gather_into_tensor"], calls
+        finally:
+            for n, f in orig.items():
+                setattr(dist, n, f)
+        assert g.device.type == "cuda" and torch.equal(g, y) and torch.equal(g2, y)
         assert shard.gather_keypoints(y) is y  # default single-rank short-circuit
     finally:
         dist.destroy_process_group()

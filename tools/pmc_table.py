@@ -32,7 +32,7 @@ def main():
     names = meta["names"]
     n = len(names)
     acc = defaultdict(lambda: defaultdict(list))
-    for sub in ("sq1", "sq2", "fetch", "write"):
+    for sub in ("sq1", "sq2", "sq3", "fetch", "write"):
         f = find(os.path.join(d, sub), "*counter_collection.csv")
         if not f:
             continue
