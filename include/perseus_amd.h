@@ -197,6 +197,22 @@ int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const do
                           const double* j_cv0, const double* j_cv1, double lambda, double* D, double* E, double* g,
                           double* delta, int32_t* info, void* ws, size_t ws_bytes, void* stream);
 
+/* Fixed-lag window of the config-4 streaming pose stage (the smoother loop the reference
+ * leaves to downstream GTSAM code; scripts/streaming.py:121-155 runs the detector only).
+ * Per trajectory t the window holds frames l = 0..L-1 of y (T*L, 2K) f32, pose (T*L, 12),
+ * angvel and vel (T*L, 3), all device, frame f = t*L + l.
+ * pa_window_advance: shifts every array one frame towards l = 0 (frame 0 dropped),
+ * writes y_new[t] (T, 2K) as frame L-1 and predicts pose[L-1] = pose[L-2] Exp(dt [w; v_b])
+ * (the PoseDynamicsFactor model, factors.py:100-105; v_b = R^T v for PA_VEL_WORLD) with
+ * angvel / vel carried over from frame L-2.
+ * pa_window_retract: pose <- pose Exp(delta[0:6]) (Pose3 retract, Expmap chart),
+ * angvel += delta[6:9], vel += delta[9:12] for pa_trajectory_gn_step's delta (T*L, 12);
+ * trajectories with info[t] != 0 are left unchanged (info may be NULL). */
+int pa_window_advance(int T, int L, int n_kp, const float* y_new_dev, float* y_dev, double* pose_dev,
+                      double* angvel_dev, double* vel_dev, double dt, int vel_frame, void* stream);
+int pa_window_retract(int T, int L, const double* delta_dev, const int32_t* info_dev, double* pose_dev,
+                      double* angvel_dev, double* vel_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -410,3 +410,47 @@ def projection_batch(Tb, p_b, z, K, Tc=None):
         r[i], J[i], st[i], _ = projection(unpack(Tb[i]), p_b[i], z[i], K,
                                           None if Tc is None else unpack(Tc))
     return r, J, st
+
+
+# -------------------------------------------------------------------------------------
+# fixed-lag window of the config-4 streaming pose stage (include/perseus_amd.h
+# pa_window_advance / pa_window_retract); the reference has no smoother loop of its own
+# (scripts/streaming.py:121-155 stops at pixels), so these restate the build's definition
+# with the reference's dynamics model (factors.py:100-105) and GTSAM's Pose3 retract
+# (Expmap chart).  Parity of these two is therefore against the build's spec, not the
+# reference.
+# -------------------------------------------------------------------------------------
+def window_advance(win: dict, y_new, dt, vel_frame="world") -> dict:
+    """win: y (T, L, 2K), pose (T, L, 12), angvel / vel (T, L, 3); returns the advanced
+    copy: frames shift one towards l = 0, y_new (T, 2K) appended, the new pose =
+    pose[L-2] Exp(dt [w; v_b]) with v_b = R^T v (world) or v (body), velocities carried."""
+    out = {k: np.array(v, copy=True) for k, v in win.items()}
+    for k in out:
+        out[k][:, :-1] = win[k][:, 1:]
+    out["y"][:, -1] = y_new
+    T, L = out["pose"].shape[:2]
+    for t in range(T):
+        T1 = unpack(out["pose"][t, L - 2])
+        w = out["angvel"][t, L - 2]
+        v = out["vel"][t, L - 2]
+        vb = T1[0].T @ v if vel_frame == "world" else v
+        out["pose"][t, L - 1] = pack(compose(T1, pose_exp(np.concatenate([dt * w, dt * vb]))))
+        out["angvel"][t, L - 1] = w
+        out["vel"][t, L - 1] = v
+    return out
+
+
+def window_retract(win: dict, delta, info=None) -> dict:
+    """pose <- pose Exp(delta[:6]), angvel += delta[6:9], vel += delta[9:12] per frame;
+    delta (T*L, 12); trajectories with info != 0 unchanged."""
+    out = {k: np.array(v, copy=True) for k, v in win.items()}
+    T, L = out["pose"].shape[:2]
+    d = np.asarray(delta).reshape(T, L, 12)
+    for t in range(T):
+        if info is not None and info[t] != 0:
+            continue
+        for l in range(L):
+            out["pose"][t, l] = pack(compose(unpack(out["pose"][t, l]), pose_exp(d[t, l, :6])))
+            out["angvel"][t, l] = out["angvel"][t, l] + d[t, l, 6:9]
+            out["vel"][t, l] = out["vel"][t, l] + d[t, l, 9:12]
+    return out

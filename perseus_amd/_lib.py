@@ -62,6 +62,11 @@ _SIGS = {
     "pa_trajectory_gn_workspace": (C.c_size_t, [C.c_int, C.c_int]),
     "pa_trajectory_gn_step": (C.c_int, [C.c_int, C.c_int, C.c_int] + [C.c_void_p] * 11 + [C.c_double]
                               + [C.c_void_p] * 6 + [C.c_size_t, C.c_void_p]),
+    "pa_window_advance": (C.c_int, [C.c_int, C.c_int, C.c_int] + [C.c_void_p] * 5 + [C.c_double, C.c_int,
+                                                                                     C.c_void_p]),
+    "pa_window_retract": (C.c_int, [C.c_int, C.c_int] + [C.c_void_p] * 6),
+    "pa_debug_gn_set_assemblers": (C.c_int, [C.c_int]),
+    "pa_debug_gn_set_trace": (C.c_int, [C.c_void_p]),
     "pa_loss_statistics_workspace": (C.c_size_t, [C.c_longlong]),
     "pa_loss_statistics": (C.c_int, [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "pa_proj_linearize": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,

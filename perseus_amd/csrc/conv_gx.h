@@ -26,17 +26,6 @@
 // (+ residual) loads; MFMAs of 2s+1; wait for what step s + 2's fragments need and
 // cross a bare s_barrier.
 //
-// KS = 2 (intra-workgroup split-K): two groups of WM x WN waves compute the same output
-// tile, group kg taking half-step kg (channels 32 kg .. 32 kg + 31 of every 64-channel
-// K-slice) of every step.  A wave's tile is twice the KS = 1 tile for the same
-// workgroup tile and wave count, so it reads half the LDS fragments per MFMA (layer3:
-// 64 px x 64 ch per wave, 0.5 ds_read_b128 per MFMA instead of 0.75; MFMA-shape
-// ubench tools/ubench/mfma_shapes.hip: 0.58 vs 0.49 of the fp16 peak).  After the K
-// loop each group hands the accumulators of the half of the tile the other group
-// finalizes through LDS (ds_write_b128, after the last fragment reads), then both
-// groups run the epilogue on their own half.  The f32 sum order differs from KS = 1
-// (each output = half-sum(kg 0) + half-sum(kg 1)), so KS = 2 is not bit-identical to it.
-//
 // X3 (the fp16x3 parity mode): activations are a pair of fp16 planes per
 // pixel, [hi (Cin) | lo (Cin)] with hi = fp16(v), lo = fp16(v - hi), and the weights
 // [tap][hi (Cin) | lo (Cin)] of w * 2^e_co (e_co per output channel, so lo stays a
@@ -258,9 +247,9 @@ __device__ __forceinline__ HiLo split_x3(float v) {
 }
 
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1,
-          bool WT = true, bool X3 = false, int KS = 1>
-__global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int xg) {
-  constexpr int NW = WM * WN * KS, NT = NW * 64;
+          bool WT = true, bool X3 = false>
+__global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
+  constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
   using VB = GxBlocks<X3, NCB>;
   constexpr int XS = X3 ? 2 : 1;  // fp16 planes per activation / weight element
@@ -283,25 +272,20 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
   static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile");
   static_assert(TW >= 16 || (TW == 8 && NI == 2), "fragment geometry");
   static_assert(G >= 1 && G <= 3 && PD >= G + 1 && PD <= 8, "prefetch distance / steps per barrier");
-  static_assert(KS == 1 || (KS == 2 && FD == 1 && TM % 2 == 0 && !(EPI & EPI_HEAD)), "split-K configuration");
-  constexpr int TMO = TM / KS;  // accumulator rows (16-pixel fragments) this wave finalizes
   // slot (t + PD) % NSLOT, written at step t, was last read by step t + PD - NSLOT,
   // which must lie before the last barrier: t - G with a barrier every G steps
   constexpr int NSLOT = PD + G;
-  constexpr int RL = XS * TN + ((EPI & EPI_RES) ? XS * TMO * TN / 2 : 0);
+  constexpr int RL = XS * TN + ((EPI & EPI_RES) ? XS * TM * TN / 2 : 0);
   // epilogue loads (bias, residual) issued RSD steps before the end: early enough to
   // land, late enough not to hold their VGPRs across the whole K loop
   constexpr int RSD = 4;
   constexpr GxPlan plan{NSTEPS, VB::NVB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G};
-  constexpr int STAGEB = 2 * PATCHB + NSLOT * WB;
-  constexpr int XCHB = (KS - 1) * WM * WN * TM * TN * 1024;  // split-K hand-over (after the K loop)
-  __shared__ __attribute__((aligned(1024))) char smem[STAGEB > XCHB ? STAGEB : XCHB];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * PATCHB + NSLOT * WB];
   char* patch = smem;
   char* wring = smem + 2 * PATCHB;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int kg = KS == 1 ? 0 : wid / (WM * WN), wpos = wid - kg * (WM * WN);
-  const int wm = wpos / WN, wn = wpos - (wpos / WN) * WN;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int q = lane >> 4, r16 = lane & 15;
   const int H = a.Hout, W = a.Wout;
   const _Float16* __restrict__ in = (const _Float16*)a.in;
@@ -381,12 +365,10 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
 
   const _Float16* __restrict__ res = (const _Float16*)a.res;
   _Float16* __restrict__ out = (_Float16*)a.out;
-  // output pixels of the TMO accumulator rows this wave finalizes (tm = kg * TMO + i)
-  size_t pixo[TMO];
-  bool ok[TMO];
+  size_t pixo[TM];
+  bool ok[TM];
 #pragma unroll
-  for (int i = 0; i < TMO; ++i) {
-    const int tm = kg * TMO + i;
+  for (int tm = 0; tm < TM; ++tm) {
     const int mb = wm * WTM + tm * 16;
     int img, y, x;
     if constexpr (TW == 8) {
@@ -399,11 +381,11 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
       x = mb % TW + o;
     }
     const int n = img0 + img;
-    ok[i] = n < a.B;
-    pixo[i] = ((((size_t)(ok[i] ? n : 0)) * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
+    ok[tm] = n < a.B;
+    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
   }
-  half8 rv[TMO][TN / 2];
-  half8 rl[X3 ? TMO : 1][TN / 2];  // X3: the residual's lo plane
+  half8 rv[TM][TN / 2];
+  half8 rl[X3 ? TM : 1][TN / 2];  // X3: the residual's lo plane
   f32x4 bias[TN];
   f32x4 scl[X3 ? TN : 1];  // X3: 2^-e per output channel
   auto load_epi = [&]() __attribute__((always_inline)) {
@@ -415,11 +397,11 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
     }
     if constexpr (EPI & EPI_RES) {
 #pragma unroll
-      for (int i = 0; i < TMO; ++i)
+      for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
         for (int p = 0; p < TN / 2; ++p) {
-          rv[i][p] = *reinterpret_cast<const half8*>(res + pixo[i] + p * 32);
-          if constexpr (X3) rl[i][p] = *reinterpret_cast<const half8*>(res + pixo[i] + Cout + p * 32);
+          rv[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + p * 32);
+          if constexpr (X3) rl[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + Cout + p * 32);
         }
     }
   };
@@ -465,45 +447,19 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
         acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[SET][tn]),
                                                              __builtin_bit_cast(half8, fb[SET][tm]), acc[tm][tn], 0, 0, 0);
   };
-  // KS = 2: a wave reads and multiplies only half-step kg of every step (wave-uniform
-  // chunk offset 4 kg), fragments one step ahead in register set S & 1
-  auto read_frags_ks = [&](auto sc) __attribute__((always_inline)) {
-    constexpr int S = decltype(sc)::value;
-    constexpr int CB = S / 9, TAP = S % 9, SET = S & 1;
-    constexpr int TOFF = (TAP / 3) * PW + (TAP % 3);
-    const char* pb = patch + (CB & 1) * PATCHB;
-    const char* wb = wring + (S % NSLOT) * WB;
-    const int ch = kg * 4 + q;
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-      fa[SET][tn] = *reinterpret_cast<const xu4*>(wb + xswz(wn * WTN + tn * 16 + r16, ch));
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) fb[SET][tm] = *reinterpret_cast<const xu4*>(pb + xswz(ppix[tm] + TOFF, ch));
-  };
   // step s + 1's data landed before the barrier that closed step s - 1, so with
   // FD = 2 both its halves are read during step s
-  if constexpr (KS == 2) {
-    read_frags_ks(xic<0>{});
-  } else {
-    read_frags(xic<0>{});
-    if constexpr (FD == 2) read_frags(xic<1>{});
-  }
+  read_frags(xic<0>{});
+  if constexpr (FD == 2) read_frags(xic<1>{});
   gx_for<0, (DBG == 3 ? 0 : NSTEPS)>([&](auto sc) __attribute__((always_inline)) {
     constexpr int S = decltype(sc)::value;
     constexpr int CB = S / 9, TAP = S % 9;
-    if constexpr (KS == 2) {
-      if constexpr (S + 1 < NSTEPS) read_frags_ks(xic<S + 1>{});
-      __builtin_amdgcn_s_setprio(1);
-      mfma(xic<2 * S + (S & 1)>{});  // register set S & 1 (NSET = 2)
-      __builtin_amdgcn_s_setprio(0);
-    } else {
     if constexpr (FD == 1) read_frags(xic<2 * S + 1>{});
     else if constexpr (S + 1 < NSTEPS) read_frags(xic<2 * S + 2>{});
     __builtin_amdgcn_s_setprio(1);
     mfma(xic<2 * S>{});
     __builtin_amdgcn_s_setprio(0);
     if constexpr (S + 1 < NSTEPS) read_frags(xic<2 * S + 1 + FD>{});
-    }
     // DMAs after this step's LDS reads (they are issued by then; see xdma16)
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + PD < NSTEPS && DBG < 2) dma_w(S + PD);
@@ -515,11 +471,9 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
       load_epi();
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (KS == 1) {
-      __builtin_amdgcn_s_setprio(1);
-      mfma(xic<2 * S + 1>{});
-      __builtin_amdgcn_s_setprio(0);
-    }
+    __builtin_amdgcn_s_setprio(1);
+    mfma(xic<2 * S + 1>{});
+    __builtin_amdgcn_s_setprio(0);
     if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS && (DBG == 0 || DBG == 4)) {
       // the next group (steps s+1 .. s+G) reads the fragments of steps up to s+G+1
       // (first half): those weight tiles and their blocks' patches must have landed
@@ -532,35 +486,13 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
   if constexpr (DBG == 4) trace_stamp(a.trace, 2);
   xwait_vm<0>();  // bias / residual (also waited for by the compiler at their use)
 
-  if constexpr (KS == 2) {
-    // split-K hand-over: every wave is past its last fragment read (barrier), then each
-    // writes the rows of its tile the other group finalizes, one 16-B slot per lane
-    // (slot (wpos, tm, tn): 1 KB, contiguous, conflict-free), and adds the ones it receives
-    __syncthreads();
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-      if (tm / TMO != kg)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          *reinterpret_cast<f32x4*>(smem + ((wpos * TM + tm) * TN + tn) * 1024 + lane * 16) = acc[tm][tn];
-    __syncthreads();
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-      if (tm / TMO == kg)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          acc[tm][tn] += *reinterpret_cast<const f32x4*>(smem + ((wpos * TM + tm) * TN + tn) * 1024 + lane * 16);
-  }
-
   if constexpr (EPI & EPI_HEAD) {
     gx_head<TH, TW, NI, BN, NT, WTM, WTN, TM, TN, EPI>(a, smem, acc, bias, rv, img0, n0, ntn, o);
     return;
   }
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
-    const int i = tm % TMO;  // compile-time: this wave's row tm (when tm / TMO == kg)
-    if (KS > 1 && tm / TMO != kg) continue;
-    if (!ok[i]) continue;
+    if (!ok[tm]) continue;
 #pragma unroll
     for (int p = 0; p < TN / 2; ++p) {
       half8 hv, lv;
@@ -569,18 +501,18 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
         const int tn = 2 * p + (j >> 2), e = j & 3;
         if constexpr (X3) {
           float v = acc[tm][tn][e] * scl[tn][e] + bias[tn][e];  // exact unscale (power of 2)
-          if constexpr (EPI & EPI_RES) v += (float)rv[i][p][j] + (float)rl[i][p][j];
+          if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j] + (float)rl[tm][p][j];
           const HiLo hl = split_x3(fmaxf(v, 0.f));
           hv[j] = hl.hi;
           lv[j] = hl.lo;
         } else {
           float v = acc[tm][tn][e] + bias[tn][e];
-          if constexpr (EPI & EPI_RES) v += (float)rv[i][p][j];
+          if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
           hv[j] = (_Float16)fmaxf(v, 0.f);
         }
       }
-      store16<WT>(out, (unsigned)((pixo[i] + p * 32) * 2), hv);
-      if constexpr (X3) store16<WT>(out, (unsigned)((pixo[i] + Cout + p * 32) * 2), lv);
+      store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), hv);
+      if constexpr (X3) store16<WT>(out, (unsigned)((pixo[tm] + Cout + p * 32) * 2), lv);
     }
   }
   if constexpr (DBG == 4) {
@@ -591,7 +523,7 @@ __global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int 
 }
 
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1,
-          bool WT = true, bool X3 = false, int KS = 1>
+          bool WT = true, bool X3 = false>
 static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES) || a.epi == (EPI_RELU | EPI_RES | EPI_HEAD),
            "gx conv: epilogue %d", a.epi);
@@ -607,7 +539,7 @@ static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
   PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "gx conv: output over 2 GB");
   PA_CHECK(!X3 || (a.scale && !(a.epi & EPI_HEAD)), "gx conv (fp16x3): scale required, no fused head");
   if (a.epi & EPI_HEAD) {
-    if constexpr (TH == 8 && TW == 8 && NI == 2 && BN == 64 && WM * WN == 8 && DBG == 0 && !X3 && KS == 1) {
+    if constexpr (TH == 8 && TW == 8 && NI == 2 && BN == 64 && WM * WN == 8 && DBG == 0 && !X3) {
       PA_CHECK(a.pool && a.cnt && a.fcw && a.fcb && a.y && a.Cout == 512, "gx conv: fused head arguments");
       hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES | EPI_HEAD, DBG, FD, WT>),
                          dim3(tiles), dim3(WM * WN * 64), 0, s, a, x);
@@ -615,11 +547,11 @@ static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
       PA_CHECK(false, "gx conv: fused head needs the 2 x 8x8 x 64-channel tile");
     }
   } else if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT, X3, KS>),
-                       dim3(tiles), dim3(WM * WN * KS * 64), 0, s, a, x);
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT, X3>),
+                       dim3(tiles), dim3(WM * WN * 64), 0, s, a, x);
   else
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT, X3, KS>), dim3(tiles),
-                       dim3(WM * WN * KS * 64), 0, s, a, x);
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT, X3>), dim3(tiles),
+                       dim3(WM * WN * 64), 0, s, a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -12,8 +12,6 @@ int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s) {
   if (variant == 7 && a.trace) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 4>(a, true, s);  // timestamps
   if (variant == 8) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 2>(a, xg, s);  // timing only
   if (variant == 9) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 3>(a, xg, s);  // timing only
-  if (variant == 5)  // split-K: 4 x 1 waves of 64 px x 64 ch, x 2 K-halves
-    return run_gx<16, 16, 1, 64, 4, 1, 256, 3, 1, 0, 1, true, false, 2>(a, xg, s);
   switch (variant & 3) {
       case 1: return run_gx<8, 16, 1, 64, 2, 2, 256, 3>(a, xg, s);  // 80 KB LDS: 2 workgroups per CU
       case 2: return run_gx<16, 16, 1, 64, 4, 2, 256, 4, 3>(a, xg, s);

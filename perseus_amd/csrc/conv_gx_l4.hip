@@ -16,10 +16,6 @@ int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s) {
   // shipped: 4 channel groups per XCD (round 2: HBM traffic 31-35 MB vs 46-51 per launch with the 1-D order,
   // time unchanged within 1 %, bit-identical)
   const int xgv = xg ? 4 : 0;
-  if (variant == 5)  // split-K: 2 x 2 waves of 64 px x 32 ch, x 2 K-halves
-    return run_gx<8, 8, 2, 64, 2, 2, 512, 4, 1, 0, 1, true, false, 2>(a, xgv, s);
-  if (variant == 6)  // split-K: 4 x 1 waves of 32 px x 64 ch, x 2 K-halves
-    return run_gx<8, 8, 2, 64, 4, 1, 512, 4, 1, 0, 1, true, false, 2>(a, xgv, s);
   switch (variant & 3) {
     case 1: return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 2>(a, xgv, s);  // barrier every 2 steps (bit-identity cross-check)
     default: return run_gx<8, 8, 2, 64, 4, 2, 512, 4>(a, xgv, s);

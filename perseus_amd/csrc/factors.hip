@@ -880,9 +880,109 @@ __global__ __launch_bounds__(128, 2) void traj_all_kernel(pa_traj_args a, int mo
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Fixed-lag window of the streaming pose stage (config 4): the smoother loop the
+// reference leaves to downstream GTSAM code (scripts/streaming.py:121-155 runs the
+// detector only), restated on device so a tick's poses never leave HBM.
+
+// Advance: one workgroup per trajectory.  Thread e moves element e of every per-frame
+// record one frame towards l = 0 (reads frame l + 1 before writing frame l: no other
+// thread touches element e), then thread 0 predicts the new last frame with the
+// PoseDynamicsFactor model (factors.py:100-105): pose[L-1] = pose[L-2] Exp(dt [w; v_b]),
+// v_b = R^T v for a world-frame velocity; angvel / vel carried over.
+__global__ __launch_bounds__(64) void window_advance_kernel(int L, int n_kp, const float* __restrict__ y_new,
+                                                            float* y, double* pose, double* angvel, double* vel,
+                                                            double dt, int vel_frame) {
+  const int t = blockIdx.x, e = threadIdx.x;
+  const int ny = 2 * n_kp;
+  float* yt = y + (size_t)t * L * ny;
+  double* pt = pose + (size_t)t * L * 12;
+  double* wt = angvel + (size_t)t * L * 3;
+  double* vt = vel + (size_t)t * L * 3;
+  for (int l = 0; l + 1 < L; ++l) {
+    if (e < ny) yt[l * ny + e] = yt[(l + 1) * ny + e];
+    if (e < 12) pt[l * 12 + e] = pt[(l + 1) * 12 + e];
+    if (e < 3) {
+      wt[l * 3 + e] = wt[(l + 1) * 3 + e];
+      vt[l * 3 + e] = vt[(l + 1) * 3 + e];
+    }
+  }
+  if (e < ny) yt[(L - 1) * ny + e] = y_new[(size_t)t * ny + e];
+  __syncthreads();
+  if (e == 0 && L >= 2) {
+    const Pose T1 = load_pose(pt + (L - 2) * 12);
+    const V3 w = load3(wt + (L - 2) * 3), v = load3(vt + (L - 2) * 3);
+    const V3 vb = vel_frame == PA_VEL_WORLD ? mtv(T1.R, v) : v;
+    const V3 xw = dt * w, xv = dt * vb;
+    const Pose P = compose(T1, pose_exp(xw, xv, ang(xw)));
+    double* o = pt + (L - 1) * 12;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o[i] = P.R.a[i];
+    o[9] = P.t.x;
+    o[10] = P.t.y;
+    o[11] = P.t.z;
+    wt[(L - 1) * 3 + 0] = w.x;
+    wt[(L - 1) * 3 + 1] = w.y;
+    wt[(L - 1) * 3 + 2] = w.z;
+    vt[(L - 1) * 3 + 0] = v.x;
+    vt[(L - 1) * 3 + 1] = v.y;
+    vt[(L - 1) * 3 + 2] = v.z;
+  }
+}
+
+// Retract: one thread per frame.  pose <- pose Exp(delta[0:6]) (GTSAM Pose3::retract
+// with the Expmap chart, tangent [omega; v]), angvel += delta[6:9], vel += delta[9:12]
+// (pa_trajectory_gn_step's variable block); trajectories whose step failed (info != 0)
+// keep their values.
+__global__ __launch_bounds__(64) void window_retract_kernel(int T, int L, const double* __restrict__ delta,
+                                                            const int32_t* __restrict__ info, double* pose,
+                                                            double* angvel, double* vel) {
+  const long f = (long)blockIdx.x * 64 + threadIdx.x;
+  if (f >= (long)T * L) return;
+  if (info && info[f / L] != 0) return;
+  const double* d = delta + f * 12;
+  const V3 dw = load3(d), dv = load3(d + 3);
+  const Pose P = compose(load_pose(pose + f * 12), pose_exp(dw, dv, ang(dw)));
+  double* o = pose + f * 12;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) o[i] = P.R.a[i];
+  o[9] = P.t.x;
+  o[10] = P.t.y;
+  o[11] = P.t.z;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    angvel[f * 3 + i] += d[6 + i];
+    vel[f * 3 + i] += d[9 + i];
+  }
+}
+
 }  // namespace pa
 
 extern "C" {
+
+int pa_window_advance(int T, int L, int n_kp, const float* y_new, float* y, double* pose, double* angvel,
+                      double* vel, double dt, int vel_frame, void* stream) {
+  PA_CHECK(T >= 0 && L >= 1 && n_kp >= 1 && n_kp <= 32, "T=%d L=%d n_kp=%d", T, L, n_kp);
+  if (T == 0) return PA_OK;
+  PA_CHECK(y_new && y && pose && angvel && vel, "null pointer");
+  PA_CHECK(vel_frame == PA_VEL_WORLD || vel_frame == PA_VEL_BODY, "vel_frame must be 'world' or 'body'.");
+  hipLaunchKernelGGL(pa::window_advance_kernel, dim3(T), dim3(64), 0, (hipStream_t)stream, L, n_kp, y_new, y, pose,
+                     angvel, vel, dt, vel_frame);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+int pa_window_retract(int T, int L, const double* delta, const int32_t* info, double* pose, double* angvel,
+                      double* vel, void* stream) {
+  PA_CHECK(T >= 0 && L >= 1, "T=%d L=%d", T, L);
+  if (T == 0) return PA_OK;
+  PA_CHECK(delta && pose && angvel && vel, "null pointer");
+  const long n = (long)T * L;
+  hipLaunchKernelGGL(pa::window_retract_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     T, L, delta, info, pose, angvel, vel);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
 
 int pa_dyn_linearize(int n, const double* t1, const double* w, const double* v, const double* t2, double dt,
                      int vel_frame, const double* inv_sigma, double* r, double* j0, double* j1, double* j2,

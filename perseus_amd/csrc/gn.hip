@@ -32,7 +32,13 @@ struct GnArgs {
   double *D, *E, *g, *delta;
   int32_t* info;
   double* ws;
+  unsigned long long* trace;  // timing only (pa_debug_gn_set_trace): 256 s_memrealtime stamps per trajectory
 };
+
+// slot s of trajectory t's trace (lane 0 of the calling wave only)
+__device__ __forceinline__ void gn_stamp(const GnArgs& a, int t, int slot) {
+  if (a.trace && (threadIdx.x & 63) == 0 && slot < 256) a.trace[(size_t)t * 256 + slot] = __builtin_amdgcn_s_memrealtime();
+}
 
 // ---------------------------------------------------------------- assembly
 // One wave, frame l (of trajectory t).  The factor rows touching x_l are stacked in
@@ -247,7 +253,26 @@ __device__ __forceinline__ void lds_store_release(int* p, int v) {
 // m - R + 1, whose E block it reads last).  Every wait is satisfied by waves of the same
 // workgroup that are already running, and the solver publishes `consumed` even for frames
 // it skips after a failed pivot, so every wave runs to its end.
-template <int RP, int NA>
+// 1 / x for x > 0: the hardware estimate + two Newton steps (f64 accurate)
+__device__ __forceinline__ double gn_rcp(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  y = y * (2.0 - x * y);
+  y = y * (2.0 - x * y);
+  return y;
+}
+
+// SOLVER = 1 (round 3): block Thomas with explicit inverses, so the per-frame chain has ONE
+// 12-step sequence instead of three (W solve, Cholesky, y solve):
+//   G_{l-1} = M_{l-1} E_{l-1}                   (M = S^-1; 12 x 12 x 12, no chain)
+//   S_l = D_l + lambda I - E_{l-1}^T G_{l-1}    (no chain)
+//   b_l = -g_l - E_{l-1}^T z_{l-1}
+//   M_l = S_l^-1 by the symmetric sweep operator (12 pivots; the pivots are S_l's LDL^T
+//          pivots, so a pivot <= 0 <=> S_l not positive definite, as the Cholesky test)
+//   z_l = M_l b_l;  backward  delta_l = z_l - G_l delta_{l+1}  (one mat-vec per frame).
+// 36 lanes hold a 12 x 12 block, lane i: row i / 3, columns 4 (i % 3) .. + 3; the sweep
+// hands row k round through LDS (one wave: LDS ops run in order) and uses symmetry for
+// column k.
+template <int RP, int NA, int SOLVER>
 __global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
   using namespace gn;
   constexpr int BLK = 2 * NB + NV;  // D | E | g of one frame
@@ -271,15 +296,179 @@ __global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
   if (wv < NA) {
     for (int l = wv; l < L; l += NA) {
       while (lds_load_acquire(&consumed) < l - R + 2) __builtin_amdgcn_s_sleep(2);
+      gn_stamp(a, t, 2 * l);  // assembler: frame l start (slot 2 l) / published (2 l + 1)
       gn_assemble_frame<RP>(a, f0 + l, st[wv], blk[l % R]);
       if (i == 0) lds_store_release(&ready[l % R], l + 1);
+      gn_stamp(a, t, 2 * l + 1);
     }
+    return;
+  }
+  double* ws = a.ws + (size_t)t * L * GN_WSF;
+  int info = 0;
+  if constexpr (SOLVER == 1) {
+    __shared__ __attribute__((aligned(16))) double bs[NV];
+    double* Mp = Lp;  // M_{l-1}, row-major
+    double* Pb = Wt;  // G_{l-1}
+    double* zp = ys;  // z_{l-1}
+    double* rowk = Ld;  // the sweep's current pivot row
+    typedef double d2_t __attribute__((ext_vector_type(2)));
+    const bool act = i < 36;
+    const int ii = act ? i : 35;
+    const int r = ii / 3, c0 = 4 * (ii - 3 * (ii / 3));
+    for (int l = 0; l < L; ++l) {
+      const int cur = l % R, prv = (l + R - 1) % R;
+      gn_stamp(a, t, 64 + 4 * l);  // solver: frame l wait start / data ready / sweep start / done
+      while (lds_load_acquire(&ready[cur]) != l + 1) __builtin_amdgcn_s_sleep(1);
+      gn_stamp(a, t, 65 + 4 * l);
+      if (!info) {
+        double* wl = ws + (size_t)l * GN_WSF;
+        const double* bc = blk[cur];
+        const double* bp = blk[prv];
+        double sv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sv[c] = bc[r * NV + c0 + c] + (r == c0 + c ? a.lambda : 0.0);
+        double b = -bc[2 * NB + r];
+        if (l > 0) {
+          // G_{l-1}[r][c0..] = sum_k M_{l-1}[r][k] E_{l-1}[k][c0..]
+          double pv[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int k = 0; k < NV; ++k) {
+            const double m = Mp[r * NV + k];
+            const d2_t e0 = *reinterpret_cast<const d2_t*>(bp + NB + k * NV + c0);
+            const d2_t e1 = *reinterpret_cast<const d2_t*>(bp + NB + k * NV + c0 + 2);
+            pv[0] += m * e0[0];
+            pv[1] += m * e0[1];
+            pv[2] += m * e1[0];
+            pv[3] += m * e1[1];
+          }
+          wave_lds_sync();  // every lane is past its reads of M_{l-1} / G_{l-2}
+          if (act) {
+            *reinterpret_cast<d2_t*>(Pb + r * NV + c0) = d2_t{pv[0], pv[1]};
+            *reinterpret_cast<d2_t*>(Pb + r * NV + c0 + 2) = d2_t{pv[2], pv[3]};
+            double* gw = ws + (size_t)(l - 1) * GN_WSF + r * NV + c0;  // G_{l-1} for the backward pass
+#pragma unroll
+            for (int c = 0; c < 4; ++c) gw[c] = pv[c];
+          }
+          wave_lds_sync();
+          // S -= E_{l-1}^T G_{l-1};  b -= E_{l-1}^T z_{l-1}
+          double s2[4] = {0.0, 0.0, 0.0, 0.0}, b2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < NV; ++k) {
+            const double ek = bp[NB + k * NV + r];
+            const d2_t p0 = *reinterpret_cast<const d2_t*>(Pb + k * NV + c0);
+            const d2_t p1 = *reinterpret_cast<const d2_t*>(Pb + k * NV + c0 + 2);
+            s2[0] += ek * p0[0];
+            s2[1] += ek * p0[1];
+            s2[2] += ek * p1[0];
+            s2[3] += ek * p1[1];
+            b2 += ek * zp[k];
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) sv[c] -= s2[c];
+          b -= b2;
+        }
+        gn_stamp(a, t, 66 + 4 * l);
+        // M_l = S_l^-1: symmetric sweep, pivot k = 0 .. 11 (ends with -S^-1)
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          wave_lds_sync();  // previous step's reads of rowk done (program order + compiler fence)
+          if (act && r == k) {
+            *reinterpret_cast<d2_t*>(rowk + c0) = d2_t{sv[0], sv[1]};
+            *reinterpret_cast<d2_t*>(rowk + c0 + 2) = d2_t{sv[2], sv[3]};
+          }
+          wave_lds_sync();
+          double piv = rowk[k];
+          const double ark = rowk[r];  // S[r][k] = S[k][r] (symmetric)
+          const d2_t k0 = *reinterpret_cast<const d2_t*>(rowk + c0);
+          const d2_t k1 = *reinterpret_cast<const d2_t*>(rowk + c0 + 2);
+          const double akj[4] = {k0[0], k0[1], k1[0], k1[1]};
+          if (!(piv > 0.0)) {
+            bad = true;
+            piv = 1.0;
+          }
+          const double ip = gn_rcp(piv);
+          const double f = ark * ip;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int j = c0 + c;
+            if (r == k)
+              sv[c] = j == k ? -ip : akj[c] * ip;
+            else if (j == k)
+              sv[c] = f;
+            else
+              sv[c] -= f * akj[c];
+          }
+        }
+        if (bad) {
+          info = l + 1;  // the solver wave idles through the remaining frames' hand-overs
+        } else {
+          wave_lds_sync();
+          if (act) {
+            *reinterpret_cast<d2_t*>(Mp + r * NV + c0) = d2_t{-sv[0], -sv[1]};
+            *reinterpret_cast<d2_t*>(Mp + r * NV + c0 + 2) = d2_t{-sv[2], -sv[3]};
+            if (c0 == 0) bs[r] = b;
+          }
+          wave_lds_sync();
+          double z0 = 0.0, z1 = 0.0;
+#pragma unroll
+          for (int j = 0; j < NV; j += 2) {
+            z0 += Mp[r * NV + j] * bs[j];
+            z1 += Mp[r * NV + j + 1] * bs[j + 1];
+          }
+          wave_lds_sync();
+          if (act && c0 == 0) {
+            zp[r] = z0 + z1;
+            wl[NB + r] = z0 + z1;
+          }
+        }
+      }
+      if (i == 0) lds_store_release(&consumed, l + 1);
+      gn_stamp(a, t, 67 + 4 * l);
+    }
+    gn_stamp(a, t, 250);
+    if (!info) {
+      // backward: delta_l = z_l - G_l delta_{l+1}; lane i < 12: row i
+      const int ir = i < NV ? i : NV - 1;
+      double* dl = bs;  // delta_{l+1}
+      double G_n[NV], z_n = ws[(size_t)(L - 1) * GN_WSF + NB + ir];
+      for (int l = L - 1; l >= 0; --l) {
+        double Gr[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) Gr[k] = G_n[k];
+        const double z = z_n;
+        if (l > 0) {  // frame l - 1's G row and z, one frame ahead
+          const double* wn = ws + (size_t)(l - 1) * GN_WSF;
+#pragma unroll
+          for (int k = 0; k < NV; ++k) G_n[k] = wn[ir * NV + k];
+          z_n = wn[NB + ir];
+        }
+        double d = z;
+        if (l + 1 < L) {
+          double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < NV; k += 2) {
+            d0 += Gr[k] * dl[k];
+            d1 += Gr[k + 1] * dl[k + 1];
+          }
+          d -= d0 + d1;
+        }
+        wave_lds_sync();
+        if (i < NV) {
+          dl[i] = d;
+          a.delta[((size_t)t * L + l) * NV + i] = d;
+        }
+        wave_lds_sync();
+      }
+    } else {
+      for (int e = i; e < L * NV; e += 64) a.delta[(size_t)t * L * NV + e] = NAN;
+    }
+    if (a.info && i == 0) a.info[t] = info;
+    gn_stamp(a, t, 251);
     return;
   }
   const int ic = i < NV ? i : NV - 1;  // lanes >= 12 shadow row / column 11 (no stores)
   const bool act = i < NV;
-  double* ws = a.ws + (size_t)t * L * GN_WSF;
-  int info = 0;
   for (int l = 0; l < L; ++l) {
     const int cur = l % R, prv = (l + R - 1) % R;
     while (lds_load_acquire(&ready[cur]) != l + 1) __builtin_amdgcn_s_sleep(1);
@@ -437,9 +626,43 @@ __global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
   if (a.info && i == 0) a.info[t] = info;
 }
 
+// assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * solver;
+// 0 = the shipped choice)
+static int g_gn_na = 0;
+static unsigned long long* g_gn_trace = nullptr;
+
+template <int RP, int SV>
+static void launch_gn_sv(const GnArgs& a, int na, hipStream_t s) {
+  switch (na) {
+    case 1: hipLaunchKernelGGL((gn_step_kernel<RP, 1, SV>), dim3(a.T), dim3(64 * 2), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((gn_step_kernel<RP, 3, SV>), dim3(a.T), dim3(64 * 4), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((gn_step_kernel<RP, 4, SV>), dim3(a.T), dim3(64 * 5), 0, s, a); break;
+    default: hipLaunchKernelGGL((gn_step_kernel<RP, 2, SV>), dim3(a.T), dim3(64 * 3), 0, s, a); break;
+  }
+}
+
+template <int RP>
+static void launch_gn(const GnArgs& a, int v, hipStream_t s) {
+  if (v & 8)
+    launch_gn_sv<RP, 1>(a, v & 7, s);
+  else
+    launch_gn_sv<RP, 0>(a, v & 7, s);
+}
+
 }  // namespace pa
 
 extern "C" {
+
+int pa_debug_gn_set_trace(unsigned long long* trace_dev) {
+  pa::g_gn_trace = trace_dev;
+  return PA_OK;
+}
+
+int pa_debug_gn_set_assemblers(int na) {
+  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 16, "gn variant %d: assembler waves (0..4) + 8 * solver (0, 1)", na);
+  pa::g_gn_na = na;
+  return PA_OK;
+}
 
 size_t pa_trajectory_gn_workspace(int T, int L) {
   return (T > 0 && L > 0) ? (size_t)T * L * pa::GN_WSF * sizeof(double) : 0;
@@ -461,13 +684,13 @@ int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const do
   PA_CHECK(ws_bytes >= pa_trajectory_gn_workspace(T, L), "gn: workspace %zu < %zu", ws_bytes,
            pa_trajectory_gn_workspace(T, L));
   const pa::GnArgs a{T,     L,      n_kp,   r_proj, j_proj, status_proj, r_dyn, j_dyn0, j_dyn1, j_dyn2, j_dyn3,
-                     r_cv,  j_cv0,  j_cv1,  lambda, D,      E,           g,     delta,  info,   (double*)ws};
+                     r_cv,  j_cv0,  j_cv1,  lambda, D,      E,           g,     delta,  info,   (double*)ws,
+                     pa::g_gn_trace};
   const hipStream_t s = (hipStream_t)stream;
-  constexpr int GN_NA = 2;  // assembler waves per trajectory
   if (n_kp == 8)
-    hipLaunchKernelGGL((pa::gn_step_kernel<34, GN_NA>), dim3(T), dim3(64 * (GN_NA + 1)), 0, s, a);
+    pa::launch_gn<34>(a, pa::g_gn_na, s);
   else
-    hipLaunchKernelGGL((pa::gn_step_kernel<2 * pa::GN_KMAX + 18, GN_NA>), dim3(T), dim3(64 * (GN_NA + 1)), 0, s, a);
+    pa::launch_gn<2 * pa::GN_KMAX + 18>(a, pa::g_gn_na, s);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -132,31 +132,77 @@ def detect_and_linearize(model, x: torch.Tensor, poses, vels, angvels, corners, 
     return out
 
 
+class GNPlan:
+    """One damped Gauss-Newton / LM step per trajectory (SURVEY.md 8f.4,
+    pa_trajectory_gn_step) over `lin` = the outputs of prepare_trajectories /
+    linearize_trajectories run with whitening sigmas and Jacobians, with every output and
+    the workspace allocated once, so `launch` can be captured in a HIP graph and replayed
+    (the streaming pose stage).  out: D (T*L,12,12), E (T*(L-1),12,12), g (T*L,12),
+    delta (T*L,12), info (T,) int32 (0 = solved).  Variable block per frame:
+    [pose (6) | angvel (3) | vel (3)]."""
+
+    def __init__(self, lin: dict, *, T: int, L: int, lam: float = 0.0):
+        if lin.get("j_proj") is None:
+            raise RuntimeError("gn_step needs the Jacobians (linearize with jacobians=True)")
+        dev = lin["r_proj"].device
+        self.T, self.L, self.lam, self.lin = T, L, float(lam), lin
+        self.n_kp = lin["r_proj"].shape[0] // (T * L) if T * L else 0
+        m = T * max(L - 1, 0)
+        self.m = m
+
+        def e(*shape, dtype=torch.float64):
+            return torch.empty(shape, dtype=dtype, device=dev)
+
+        self.out = {"D": e(T * L, 12, 12), "E": e(max(m, 1), 12, 12), "g": e(T * L, 12), "delta": e(T * L, 12),
+                    "info": e(T, dtype=torch.int32)}
+        L_ = _lib.lib()
+        self.ws = torch.empty(max(int(L_.pa_trajectory_gn_workspace(T, L)), 8), dtype=torch.uint8, device=dev)
+        self.dev = dev
+
+    def launch(self) -> None:
+        """One pa_trajectory_gn_step on the device's current stream."""
+        lin, out, p = self.lin, self.out, _lib.ptr
+        with torch.cuda.device(self.dev):
+            _lib.check(_lib.lib().pa_trajectory_gn_step(
+                self.T, self.L, self.n_kp, p(lin["r_proj"]), p(lin["j_proj"]), p(lin.get("status")), p(lin["r_dyn"]),
+                p(lin["j_dyn0"]), p(lin["j_dyn1"]), p(lin["j_dyn2"]), p(lin["j_dyn3"]), p(lin["r_cv"]),
+                p(lin["j_cv0"]), p(lin["j_cv1"]), self.lam, p(out["D"]), p(out["E"]), p(out["g"]), p(out["delta"]),
+                p(out["info"]), p(self.ws), self.ws.numel(), _lib.stream_of(self.dev)), "pa_trajectory_gn_step")
+
+
 def gn_step(lin: dict, *, T: int, L: int, lam: float = 0.0) -> dict:
     """One damped Gauss-Newton / LM step per trajectory on the device (SURVEY.md 8f.4,
     pa_trajectory_gn_step) from `linearize_trajectories(...)` run with whitening sigmas and
     Jacobians.  Returns D (T*L,12,12), E (T*(L-1),12,12), g (T*L,12), delta (T*L,12) and
     info (T,) int32 (0 = solved).  Variable block per frame: [pose (6) | angvel (3) | vel (3)]."""
-    if lin.get("j_proj") is None:
-        raise RuntimeError("gn_step needs the Jacobians (linearize with jacobians=True)")
-    dev = lin["r_proj"].device
-    n_kp = lin["r_proj"].shape[0] // (T * L) if T * L else 0
-    m = T * max(L - 1, 0)
-
-    def e(*shape, dtype=torch.float64):
-        return torch.empty(shape, dtype=dtype, device=dev)
-
-    out = {"D": e(T * L, 12, 12), "E": e(max(m, 1), 12, 12), "g": e(T * L, 12), "delta": e(T * L, 12),
-           "info": e(T, dtype=torch.int32)}
-    L_ = _lib.lib()
-    ws = torch.empty(max(int(L_.pa_trajectory_gn_workspace(T, L)), 8), dtype=torch.uint8, device=dev)
-    p = _lib.ptr
-    with torch.cuda.device(dev):
-        _lib.check(L_.pa_trajectory_gn_step(
-            T, L, n_kp, p(lin["r_proj"]), p(lin["j_proj"]), p(lin.get("status")), p(lin["r_dyn"]), p(lin["j_dyn0"]),
-            p(lin["j_dyn1"]), p(lin["j_dyn2"]), p(lin["j_dyn3"]), p(lin["r_cv"]), p(lin["j_cv0"]), p(lin["j_cv1"]),
-            float(lam), p(out["D"]), p(out["E"]), p(out["g"]), p(out["delta"]), p(out["info"]), p(ws), ws.numel(),
-            _lib.stream_of(dev)), "pa_trajectory_gn_step")
-    out["E"] = out["E"][:m]
-    out["_ws"] = ws
+    plan = GNPlan(lin, T=T, L=L, lam=lam)
+    plan.launch()
+    out = dict(plan.out)
+    out["E"] = out["E"][:plan.m]
+    out["_ws"] = plan.ws
     return out
+
+
+def window_advance(y_new: torch.Tensor, win: dict, *, dt: float, vel_frame: str = "world") -> None:
+    """pa_window_advance on the device's current stream: every trajectory's window
+    (win: y (T, L, 2K) f32, pose (T, L, 12), angvel / vel (T, L, 3) f64) moves one frame,
+    y_new (T, 2K) becomes its last frame, whose pose is predicted by the
+    PoseDynamicsFactor model (factors.py:100-105)."""
+    T, L, ny = win["y"].shape
+    dev = win["y"].device
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pa_window_advance(
+            T, L, ny // 2, y_new.data_ptr(), win["y"].data_ptr(), win["pose"].data_ptr(), win["angvel"].data_ptr(),
+            win["vel"].data_ptr(), float(dt), _lib.VEL_WORLD if vel_frame == "world" else _lib.VEL_BODY,
+            _lib.stream_of(dev)), "pa_window_advance")
+
+
+def window_retract(win: dict, delta: torch.Tensor, info: torch.Tensor | None = None) -> None:
+    """pa_window_retract on the device's current stream: pose <- pose Exp(delta[:6]),
+    angvel += delta[6:9], vel += delta[9:12]; trajectories with info != 0 unchanged."""
+    T, L = win["pose"].shape[:2]
+    dev = win["pose"].device
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pa_window_retract(T, L, delta.data_ptr(), _lib.ptr(info), win["pose"].data_ptr(),
+                                                win["angvel"].data_ptr(), win["vel"].data_ptr(), _lib.stream_of(dev)),
+                   "pa_window_retract")

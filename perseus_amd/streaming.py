@@ -1,18 +1,29 @@
-"""Config 4: multi-camera streaming keypoint inference with a captured HIP graph.
+"""Config 4: multi-camera streaming keypoint inference -> pose, one captured HIP graph.
 
 Mirrors the per-frame loop of `scripts/streaming.py:120-131` (grab BGR + depth,
 `/255`, depth nan/inf -> 0 and `/0.035`, centre 256x256 crop, `model(x)`, kornia
-denormalize) for `n_cams` cameras per tick, batched into one forward.  Per tick:
+denormalize) for `n_cams` cameras per tick, batched into one forward, and (with
+`pose_window` = L > 0) the pose stage BASELINE.json configs[4] asks for ("end-to-end pose
+latency"): a fixed-lag smoother per camera over its last L frames built from the
+reference's own factors (perseus/smoother/factors.py: KeypointProjectionFactor :182-275
+per keypoint, PoseDynamicsFactor :8-142 and ConstantVelocityFactor :145-171 per frame
+pair).  The reference stops at pixels (streaming.py draws them); the factor graph and
+its optimizer live in downstream GTSAM code, so this build defines the loop: one damped
+Gauss-Newton step per tick.  Per tick:
 
   host: frames -> pinned staging (centre crop rows only, or the full frame)
   GPU (one hipGraph replay on a private stream): H2D -> pa_detector_forward_rgbd
        (B = n_cams; the preprocess runs inside the stem's row loads; fp32: pa_preprocess_rgbd
        + pa_detector_forward) -> pa_keypoints_postprocess -> D2H pixels
-  host: wait for the replay, return (n_cams, K, 2) pixel coordinates.
+       [pose stage] -> pa_window_advance (window shifts one frame, the new keypoints
+       appended, the new pose predicted by the dynamics model) -> pa_trajectory_linearize
+       (whitened factors of every camera's window) -> pa_trajectory_gn_step ->
+       pa_window_retract (pose Exp(delta), velocities += delta) -> D2H newest poses + info
+  host: wait for the replay, return (n_cams, K, 2) pixel coordinates (and the poses).
 
-The graph removes the per-launch CPU cost of the ~22 launches (the forward at B=3
-is launch-bound, not compute-bound).  Workspace is reserved before capture so no
-allocation happens inside the graph.
+The graph removes the per-launch CPU cost of the ~26 launches (the forward at B=3
+is launch-bound, not compute-bound).  Workspace and every pose-stage buffer are
+allocated before capture so no allocation happens inside the graph.
 """
 
 from __future__ import annotations
@@ -20,14 +31,25 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, pipeline, synth
 
 
 class StreamingPipeline:
+    """pose_window = L > 0 turns the pose stage on (module docstring).  Its parameters:
+    K (fx, fy, s, u0, v0) of the 256x256 crop and the body-frame corners (defaults: the
+    datagen camera and cube, synth.CAMERA_K / CUBE_CORNERS); dt = the camera period;
+    sigmas of the diagonal noise models (pixels, dynamics tangent, velocity); lam = the
+    LM damping; init_pose (n_cams, 12) / init_vel / init_angvel fill every frame of the
+    initial window (default: the cube 0.4 m in front of each camera, at rest)."""
+
     def __init__(self, model, n_cams: int = 3, src_hw=(720, 1280), bgr: bool = True, host_crop: bool = True,
-                 graph: bool = True, near: float | None = None, far: float | None = None, device=None):
+                 graph: bool = True, near: float | None = None, far: float | None = None, device=None,
+                 pose_window: int = 0, K=None, corners=None, dt: float = 1.0 / 30.0, vel_frame: str = "world",
+                 proj_sigma: float = 1.0, dyn_sigma: float = 0.1, cv_sigma: float = 0.1, lam: float = 1e-2,
+                 init_pose=None, init_vel=None, init_angvel=None):
         if not torch.cuda.is_available():
             raise RuntimeError("StreamingPipeline needs a ROCm GPU (no CPU fallback)")
+        cam_K = K  # (the name K is the keypoint count below)
         self.dev = torch.device(device or torch.device("cuda", torch.cuda.current_device()))
         self.model = model
         self.n = n_cams
@@ -62,10 +84,16 @@ class StreamingPipeline:
         _lib.check(L.pa_detector_reserve(self._h, n), "reserve")
         if model.num_channels != 4:
             raise ValueError("StreamingPipeline feeds RGBD (num_channels=4)")
+        self.pose_L = int(pose_window)
+        if self.pose_L:
+            self._init_pose_stage(cam_K, corners, dt, vel_frame, proj_sigma, dyn_sigma, cv_sigma, lam, init_pose,
+                                  init_vel, init_angvel)
         self.graph = None
         with torch.cuda.stream(self.stream):
             self._enqueue()  # eager warm-up (also builds the kernels' first-launch state)
         self.stream.synchronize()
+        if self.pose_L:
+            self.reset_window()  # the warm-up tick advanced it
         if graph:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=self.stream):
@@ -90,7 +118,59 @@ class StreamingPipeline:
         _lib.check(L.pa_keypoints_postprocess(self.y.data_ptr(), None, self.n, self.model.n_keypoints, self.H, self.W,
                                               self.px_d.data_ptr(), None, s), "postprocess")
         self.px_h.copy_(self.px_d, non_blocking=True)
+        if self.pose_L:  # the pose stage, all on this stream (HBM-resident window)
+            pipeline.window_advance(self.y, self.win, dt=self.dt, vel_frame=self.vel_frame)
+            pipeline.launch(self.traj_args, self.dev)
+            self.gn.launch()
+            pipeline.window_retract(self.win, self.gn.out["delta"], self.gn.out["info"])
+            self.pose_d.copy_(self.win["pose"][:, -1])
+            self.pose_h.copy_(self.pose_d, non_blocking=True)
+            self.info_h.copy_(self.gn.out["info"], non_blocking=True)
 
+    def _init_pose_stage(self, K, corners, dt, vel_frame, proj_sigma, dyn_sigma, cv_sigma, lam, init_pose, init_vel,
+                         init_angvel):
+        n, Lw, nk, dev = self.n, self.pose_L, self.model.n_keypoints, self.dev
+        if Lw < 2:
+            raise ValueError("pose_window must be >= 2 frames (the dynamics factors couple frame pairs)")
+        if vel_frame not in ("world", "body"):
+            raise AssertionError("vel_frame must be 'world' or 'body'.")  # factors.py:41
+        self.dt, self.vel_frame = float(dt), vel_frame
+        K = synth.CAMERA_K if K is None else np.asarray(K, np.float64)
+        corners = synth.CUBE_CORNERS[:nk] if corners is None else np.asarray(corners, np.float64)
+        if init_pose is None:
+            init_pose = np.tile(np.array([1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0.4], np.float64), (n, 1))
+        zeros = np.zeros((n, 3))
+        self._init = {"pose": np.asarray(init_pose, np.float64).reshape(n, 12),
+                      "vel": np.asarray(zeros if init_vel is None else init_vel, np.float64).reshape(n, 3),
+                      "angvel": np.asarray(zeros if init_angvel is None else init_angvel, np.float64).reshape(n, 3)}
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.win = {"y": torch.zeros((n, Lw, 2 * nk), dtype=torch.float32, device=dev),
+                    "pose": torch.empty((n, Lw, 12), **f64), "angvel": torch.empty((n, Lw, 3), **f64),
+                    "vel": torch.empty((n, Lw, 3), **f64)}
+        self.traj_args, self.lin = pipeline.prepare_trajectories(
+            self.win["y"].view(n * Lw, 2 * nk), self.win["pose"].view(n * Lw, 12), self.win["vel"].view(n * Lw, 3),
+            self.win["angvel"].view(n * Lw, 3), corners, K, T=n, L=Lw, dt=self.dt, vel_frame=vel_frame, H=self.H,
+            W=self.W, proj_sigmas=[proj_sigma] * 2, dyn_sigmas=[dyn_sigma] * 6, cv_sigmas=[cv_sigma] * 3)
+        for k in ("y", "pose", "vel", "angvel"):  # linearize reads the window in place, no staging copy
+            assert self.lin["_keep"][("y", "pose", "vel", "angvel").index(k)].data_ptr() == self.win[k].data_ptr()
+        self.gn = pipeline.GNPlan(self.lin, T=n, L=Lw, lam=lam)
+        self.pose_d = torch.empty((n, 12), **f64)
+        self.pose_h = torch.empty((n, 12), dtype=torch.float64).pin_memory()
+        self.info_h = torch.empty((n,), dtype=torch.int32).pin_memory()
+
+    def reset_window(self) -> None:
+        """Every frame of every camera's window back to the initial state (keypoints 0)."""
+        with torch.cuda.stream(self.stream):
+            self.win["y"].zero_()
+            for k in ("pose", "vel", "angvel"):
+                self.win[k].copy_(torch.as_tensor(self._init[k], device=self.dev)[:, None, :]
+                                  .expand_as(self.win[k]))
+        self.stream.synchronize()
+
+    def window_state(self) -> dict:
+        """Host copies of the window (y, pose, vel, angvel) after the last tick."""
+        self.stream.synchronize()
+        return {k: v.cpu().numpy().copy() for k, v in self.win.items()}
     def stage(self, rgb: np.ndarray, depth: np.ndarray) -> None:
         """Copy one tick of camera frames (n, Hs, Ws, 3) uint8 + (n, Hs, Ws) f32 metres
         into the pinned staging buffers (centre crop only when host_crop)."""
@@ -117,6 +197,14 @@ class StreamingPipeline:
     def __call__(self, rgb: np.ndarray, depth: np.ndarray) -> np.ndarray:
         self.stage(rgb, depth)
         return self.run()
+
+    def tick(self, rgb: np.ndarray, depth: np.ndarray):
+        """One camera tick through the pose stage: (pixels (n, K, 2), newest pose of each
+        camera's window (n, 12: R row-major, t), GN info (n,) int32, 0 = solved)."""
+        if not self.pose_L:
+            raise RuntimeError("tick() needs the pose stage (pose_window > 0)")
+        px = self(rgb, depth)
+        return px, self.pose_h.numpy().copy(), self.info_h.numpy().copy()
 
     def close(self) -> None:
         """Drop the graph, then the handle it captured."""

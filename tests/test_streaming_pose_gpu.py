@@ -1,0 +1,113 @@
+"""Config 4 pose stage (BASELINE.json configs[4] "end-to-end pose latency"): the
+StreamingPipeline tick with pose_window > 0 runs detector -> window advance ->
+trajectory linearize (the reference's three factors, perseus/smoother/factors.py) ->
+GN step -> retract in ONE captured graph.
+
+  * graph replay == eager composition, bit for bit, over a sequence of ticks;
+  * one tick's chain against the oracle: oracle window advance of the previous window
+    state with the tick's keypoints, the f64 factor restatement (factors_ref) of that
+    window, the dense GN oracle (gn_ref) of the device's whitened factors, and the
+    oracle retract of the advanced window by the device's delta, against the window the
+    tick leaves behind.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import factors_ref as F
+from oracle import gn_ref as G
+from perseus_amd import synth
+from perseus_amd.detector import KeypointCNN
+from perseus_amd.streaming import StreamingPipeline
+
+from test_pipeline_gpu import _cmp, _oracle  # tests/ is on sys.path (rootdir conftest)
+from test_streaming_gpu import _frames
+
+pytestmark = pytest.mark.gpu
+LW = 6
+SIG = dict(proj_sigma=40.0, dyn_sigma=0.1, cv_sigma=0.5, lam=1e-2)
+
+
+@pytest.fixture(scope="module")
+def model():
+    m = KeypointCNN(num_channels=4)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
+    return m
+
+
+def _init(n=3):
+    rng = np.random.default_rng(5)
+    poses = []
+    for _ in range(n):
+        R, _ = F.pose_exp(np.concatenate([0.3 * rng.standard_normal(3), np.zeros(3)]))
+        poses.append(F.pack((R, np.array([0.01, -0.02, 0.35]))))
+    return np.array(poses), 0.05 * rng.standard_normal((n, 3)), 0.5 * rng.standard_normal((n, 3))
+
+
+def _pipe(model, graph):
+    p0, v0, w0 = _init()
+    return StreamingPipeline(model, graph=graph, pose_window=LW, init_pose=p0, init_vel=v0, init_angvel=w0, **SIG)
+
+
+def test_pose_graph_matches_eager(model):
+    g, e = _pipe(model, True), _pipe(model, False)
+    for seed in range(1, LW + 4):  # past a full window
+        rgb, d = _frames(seed)
+        pg, qg, ig = g.tick(rgb, d)
+        pe, qe, ie = e.tick(rgb, d)
+        np.testing.assert_array_equal(pg, pe)
+        np.testing.assert_array_equal(qg, qe)
+        np.testing.assert_array_equal(ig, ie)
+    for k, v in g.window_state().items():
+        np.testing.assert_array_equal(v, e.window_state()[k], err_msg=k)
+    assert np.isfinite(qg).all()
+    g.close()
+    e.close()
+
+
+def test_pose_tick_chain_vs_oracle(model):
+    p = _pipe(model, True)
+    for seed in range(1, LW):  # fill most of the window with real ticks
+        p.tick(*_frames(seed))
+    before = p.window_state()
+    px, pose, info = p.tick(*_frames(99))
+    after = p.window_state()
+    y_new = p.y.cpu().numpy()
+    n, nk = 3, model.n_keypoints
+    # 1. advance (the window the factors were linearized on)
+    adv = F.window_advance(before, y_new, p.dt, "world")
+    np.testing.assert_array_equal(adv["y"], after["y"])  # keypoints are only moved, never recomputed
+    # 2. factors of the advanced window, whitened as the pipeline whitens them
+    ref = _oracle(adv["pose"].reshape(-1, 12), adv["vel"].reshape(-1, 3), adv["angvel"].reshape(-1, 3),
+                  adv["y"].reshape(-1, 2 * nk), n, LW, p.dt, "world")
+    sp, sd, sc = SIG["proj_sigma"], SIG["dyn_sigma"], SIG["cv_sigma"]
+    ref["r_proj"], ref["j_proj"] = ref["r_proj"] / sp, ref["j_proj"] / sp
+    for k in ("r_dyn", "j_dyn0", "j_dyn1", "j_dyn2", "j_dyn3"):
+        ref[k] = ref[k] / sd
+    ref["r_cv"] = ref["r_cv"] / sc
+    lin = {k: (v.transpose(1, 2) if k.startswith("j_") else v) for k, v in p.lin.items()
+           if isinstance(v, torch.Tensor)}
+    _cmp(lin, ref)
+    # 3. the GN step on the device's own whitened factors
+    f = {k: lin[k].cpu().numpy() for k in ("r_proj", "j_proj", "status", "r_dyn", "j_dyn0", "j_dyn1", "j_dyn2",
+                                           "j_dyn3", "r_cv", "j_cv0", "j_cv1")}
+    _, _, d = G.gn_step(f, n, LW, nk, SIG["lam"])
+    dd = p.gn.out["delta"].cpu().numpy()
+    assert (info == 0).all()
+    np.testing.assert_allclose(dd.reshape(n, -1), d, rtol=1e-7, atol=1e-9 * np.abs(d).max())
+    # 4. retract of the advanced window by the device's delta = the window the tick left
+    ret = F.window_retract(adv, dd, info)
+    for k in ("pose", "vel", "angvel"):
+        np.testing.assert_allclose(after[k], ret[k], rtol=0, atol=1e-12, err_msg=k)
+    # the newest poses the tick returned are the window's last frames
+    np.testing.assert_array_equal(pose, after["pose"][:, -1])
+    # and the pixels are the tick's keypoints, denormalized
+    assert px.shape == (n, nk, 2)
+    p.close()
+
+
+def test_pose_window_rejects_bad_config(model):
+    with pytest.raises(ValueError):
+        StreamingPipeline(model, pose_window=1)
+    with pytest.raises(AssertionError):
+        StreamingPipeline(model, pose_window=4, vel_frame="camera")

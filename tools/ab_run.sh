@@ -1,7 +1,10 @@
+# interleaved A/B of kernel variants (tools/layer_ab.py); each step under its own time limit
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u tools/layer_ab.py --variants 0 55 --layers 2 3 4 --rounds 8 > gpurun_out/r03_ab_ks2.log 2>&1 && \
-timeout -k 10 200 python -u tools/layer_ab.py --variants 0 56 --layers 4 --rounds 8 >> gpurun_out/r03_ab_ks2.log 2>&1
-rc=$?
-cat gpurun_out/r03_ab_ks2.log
-exit $rc
+OUT=gpurun_out/${AB_TAG:-ab}.log
+: > $OUT
+for spec in "$@"; do  # spec = "LAYERS:VARIANTS", e.g. "4:0,55,56"
+  L=${spec%%:*}; V=${spec#*:}
+  timeout -k 10 300 python -u tools/layer_ab.py --variants ${V//,/ } --layers ${L//,/ } --rounds ${AB_ROUNDS:-8} >> $OUT 2>&1 || { cat $OUT; exit 1; }
+done
+cat $OUT
