@@ -30,8 +30,8 @@ int pa_detector_debug_set_trace(pa_detector* d, unsigned long long* trace_dev);
 int pa_debug_trajectory_linearize(const pa_traj_args* args, int mode, unsigned long long* trace_dev, void* stream);
 
 /* Timing only: pa_trajectory_gn_step variant = assembler waves per trajectory (1..4; 0 =
- * the shipped count) + 8 x solver (0: block Cholesky, 1: block Thomas with swept
- * inverses).  Process-wide. */
+ * the shipped count) + 8 to select the round-2 block-Cholesky solver instead of the
+ * shipped block Thomas with swept inverses.  Process-wide. */
 int pa_debug_gn_set_assemblers(int na);
 /* Timing only: pa_trajectory_gn_step writes s_memrealtime stamps (100 MHz), 256 per
  * trajectory, to trace_dev (assembler frame l: slots 2l, 2l+1; solver frame l: 64+4l ..

@@ -8,11 +8,14 @@
 //   D_l (diagonal): the K projection factors of frame l (pose), the dynamics factors
 //                   (l-1, l) and (l, l+1), the constant-velocity factors around l;
 //   E_l (x_l rows, x_{l+1} cols): the dynamics and constant-velocity factors (l, l+1).
-// One launch (gn_step_kernel), one two-wave workgroup per trajectory: wave 0 assembles
-// D_l, E_l, g_l = J^T r of frame l + 1 from the factors touching it (each block has one
-// writer, no atomics) into an LDS ring while wave 1 factors frame l -- block Cholesky
-// (L_l L_l^T = D_l + lambda I - W_l^T W_l, W_l = L_{l-1}^{-1} E_{l-1}), forward and back
-// substitution.  D / E / g are also written out (the API's outputs).  f64 throughout.
+// One launch (gn_step_kernel), one three-wave workgroup per trajectory: two assembler
+// waves (frames l = a mod 2) build D_l, E_l, g_l = J^T r from the factors touching frame
+// l (each block has one writer, no atomics) into an LDS ring while the solver wave
+// eliminates frame by frame -- SOLVER 0: block Cholesky (L_l L_l^T = D_l + lambda I -
+// W_l^T W_l, W_l = L_{l-1}^{-1} E_{l-1}) with forward and back substitution; SOLVER 1:
+// block Thomas with the Schur complements inverted by the symmetric sweep operator (one
+// 12-step chain per frame instead of three).  D / E / g are also written out (the API's
+// outputs).  f64 throughout.
 // Jacobians are column-major per factor (include/perseus_amd.h).
 #include "common.h"
 
@@ -57,147 +60,181 @@ constexpr int GN_WSF = 2 * gn::NB + 2 * gn::NV;  // workspace doubles per frame:
 // wave-local LDS ordering (one wave's ds ops run in order; the wait and the "memory" clobber
 // keep the compiler from moving LDS accesses across it)
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// compiler-only fence: one wave's LDS instructions execute in issue order, so a read
+// issued after another lane's write of the same wave sees it without a wait; this only
+// keeps the compiler from moving LDS accesses across it
+__device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
 
+// RP factor rows padded to whole 4-row MFMA k-steps (the pad rows stay zero)
 template <int RP>
 struct GnStage {
-  double AT[gn::NV][RP];
-  double rT[RP];
-  double ANT[gn::NV][10];
-  double BT[gn::NV][10];
+  static constexpr int RPP = (RP + 3) / 4 * 4;
+  double AT[gn::NV][RPP];
+  double rT[RPP];
+  double ANT[gn::NV][12];
+  double BT[gn::NV][12];
 };
+
+static __device__ int32_t gn_zero_i32[1];  // status source when no status array is given (zero-initialised)
 
 // Assembles frame f (of trajectory t, frame index l) with one wave: D_l, E_l (if l + 1 < L)
 // and g_l to the outputs a.D / a.E / a.g and to the LDS block `blk` (D | E | g).
 template <int RP>
 __device__ __forceinline__ void gn_assemble_frame(const GnArgs& a, long f, GnStage<RP>& st, double* blk) {
   using namespace gn;
-  double(&AT)[NV][RP] = st.AT;
-  double(&rT)[RP] = st.rT;
-  double(&ANT)[NV][10] = st.ANT;
-  double(&BT)[NV][10] = st.BT;
+  constexpr int RPP = GnStage<RP>::RPP;
+  double(&AT)[NV][RPP] = st.AT;
+  double(&rT)[RPP] = st.rT;
+  double(&ANT)[NV][12] = st.ANT;
+  double(&BT)[NV][12] = st.BT;
   const int lane = threadIdx.x & 63;
   const int t = (int)(f / a.L), l = (int)(f - (long)t * a.L);
   const int npair = a.L - 1;
   const int K = a.K;
   const bool nxt = l + 1 < a.L, prv = l > 0;
-  for (int e = lane; e < NV * RP; e += 64) (&AT[0][0])[e] = 0.0;
-  for (int e = lane; e < NV * 10; e += 64) {
+  // ---- loads: every value of the frame is fetched before any is used, from addresses
+  // clamped to valid elements, then selected -- one memory latency per frame (branches
+  // around guarded loads made the compiler wait out each load in turn: ~10 round trips)
+  constexpr int KM = (RP - 18) / 2;        // keypoints this instantiation holds
+  constexpr int JR = (KM * 12 + 63) / 64;  // projection Jacobian entries per lane
+  const long fk = f * K;
+  // (the status pointer test is uniform; no loaded value decides a branch before the
+  // last load is issued)
+  const bool has_st = a.st_proj != nullptr;
+  const int32_t* stp = has_st ? a.st_proj : gn_zero_i32;  // always a valid address
+  double jv[JR];
+  int js[JR];
+#pragma unroll
+  for (int q = 0; q < JR; ++q) {
+    const int e = lane + 64 * q;
+    const bool v = e < K * 12;
+    const long u = fk + (v ? e / 12 : 0);
+    jv[q] = a.j_proj[v ? fk * 12 + e : fk * 12];  // (u, c, row) = (e / 12, (e % 12) / 2, e & 1)
+    js[q] = stp[has_st ? u : 0];
+  }
+  const bool vr = lane < 2 * K;
+  const long ur = fk + (vr ? lane >> 1 : 0);
+  const double rv = a.r_proj[vr ? fk * 2 + lane : fk * 2];
+  const int rs = stp[has_st ? ur : 0];
+  // pair factors: lane classes [0, 36) dynamics J (6 x 6 column-major; < 18 also the 6 x 3
+  // J1 / J2), [36, 45) constant velocity (3 x 3), [45, 51) dynamics r, [51, 54) const-vel r
+  double n0 = 0.0, n3 = 0.0, n1 = 0.0, n2 = 0.0, p3 = 0.0;
+  if (npair > 0) {
+    const long un = (long)t * npair + (nxt ? l : 0), up = (long)t * npair + (prv ? l - 1 : 0);
+    const int e36 = lane < 36 ? lane : 0, e9 = lane >= 36 && lane < 45 ? lane - 36 : 0;
+    const int e6 = lane >= 45 && lane < 51 ? lane - 45 : 0, e3 = lane >= 51 && lane < 54 ? lane - 51 : 0;
+    const int cls = lane < 36 ? 0 : lane < 45 ? 1 : lane < 51 ? 2 : lane < 54 ? 3 : 4;
+    // per lane: the (l, l+1) factor's A-part value, its B-part value, and the (l-1, l) B-part
+    const double* sa = cls == 0 ? a.j0 + un * 36 + e36 : cls == 1 ? a.jc0 + un * 9 + e9
+                     : cls == 2 ? a.r_dyn + un * 6 + e6 : cls == 3 ? a.r_cv + un * 3 + e3 : a.j0;
+    const double* sb = cls == 0 ? a.j3 + un * 36 + e36 : cls == 1 ? a.jc1 + un * 9 + e9 : a.j3;
+    const double* sp = cls == 0 ? a.j3 + up * 36 + e36 : cls == 1 ? a.jc1 + up * 9 + e9
+                     : cls == 2 ? a.r_dyn + up * 6 + e6 : cls == 3 ? a.r_cv + up * 3 + e3 : a.j3;
+    const int e18 = lane < 18 ? lane : 0;
+    n0 = *sa;
+    n3 = *sb;
+    p3 = *sp;
+    n1 = a.j1[un * 18 + e18];
+    n2 = a.j2[un * 18 + e18];
+  }
+  // ---- staging: zero, then fill (one wave: its LDS ops run in order)
+  for (int e = lane; e < NV * RPP; e += 64) (&AT[0][0])[e] = 0.0;
+  for (int e = lane; e < NV * 12; e += 64) {
     (&ANT[0][0])[e] = 0.0;
     (&BT[0][0])[e] = 0.0;
   }
-  for (int e = lane; e < RP; e += 64) rT[e] = 0.0;
-  wave_lds_sync();
+  for (int e = lane; e < RPP; e += 64) rT[e] = 0.0;
+  wave_order();
   // projections: rows 2k, 2k + 1; J column-major 2 x 6
-  for (int e = lane; e < K * 12; e += 64) {
-    const int k = e / 12, c = (e - k * 12) >> 1, row = e & 1;
-    const long u = f * K + k;
-    if (!a.st_proj || a.st_proj[u] == 0) AT[c][2 * k + row] = a.j_proj[u * 12 + c * 2 + row];
+#pragma unroll
+  for (int q = 0; q < JR; ++q) {
+    const int e = lane + 64 * q;
+    if (e < K * 12) {
+      const int k = e / 12, c = (e - k * 12) >> 1, row = e & 1;
+      AT[c][2 * k + row] = js[q] == 0 ? jv[q] : 0.0;
+    }
   }
-  for (int e = lane; e < K * 2; e += 64) {
-    const long u = f * K + (e >> 1);
-    if (!a.st_proj || a.st_proj[u] == 0) rT[e] = a.r_proj[u * 2 + (e & 1)];
-  }
+  if (vr) rT[lane] = rs == 0 ? rv : 0.0;
   const int rn = 2 * K, rp = rn + 9;  // first row of the (l, l+1) / (l-1, l) blocks
   if (nxt) {
-    const long u = (long)t * npair + l;
     if (lane < 36) {  // dynamics: 6 x 6 / 6 x 3 / 6 x 3, column-major
       const int c = lane / 6, row = lane - c * 6;
-      const double j0 = a.j0[u * 36 + lane];
-      AT[c][rn + row] = j0;
-      ANT[c][row] = j0;
-      BT[c][row] = a.j3[u * 36 + lane];
+      AT[c][rn + row] = n0;
+      ANT[c][row] = n0;
+      BT[c][row] = n3;
       if (lane < 18) {
-        const double j1 = a.j1[u * 18 + lane], j2 = a.j2[u * 18 + lane];
-        AT[6 + c][rn + row] = j1;
-        ANT[6 + c][row] = j1;
-        AT[9 + c][rn + row] = j2;
-        ANT[9 + c][row] = j2;
+        AT[6 + c][rn + row] = n1;
+        ANT[6 + c][row] = n1;
+        AT[9 + c][rn + row] = n2;
+        ANT[9 + c][row] = n2;
       }
     } else if (lane < 45) {  // const velocity: 3 x 3 on the velocity block
       const int e = lane - 36, c = e / 3, row = e - c * 3;
-      const double c0 = a.jc0[u * 9 + e];
-      AT[9 + c][rn + 6 + row] = c0;
-      ANT[9 + c][6 + row] = c0;
-      BT[9 + c][6 + row] = a.jc1[u * 9 + e];
+      AT[9 + c][rn + 6 + row] = n0;
+      ANT[9 + c][6 + row] = n0;
+      BT[9 + c][6 + row] = n3;
     } else if (lane < 51) {
-      rT[rn + lane - 45] = a.r_dyn[u * 6 + lane - 45];
+      rT[rn + lane - 45] = n0;
     } else if (lane < 54) {
-      rT[rn + 6 + lane - 51] = a.r_cv[u * 3 + lane - 51];
+      rT[rn + 6 + lane - 51] = n0;
     }
   }
   if (prv) {
-    const long u = (long)t * npair + l - 1;
     if (lane < 36) {
       const int c = lane / 6, row = lane - c * 6;
-      AT[c][rp + row] = a.j3[u * 36 + lane];
+      AT[c][rp + row] = p3;
     } else if (lane < 45) {
       const int e = lane - 36, c = e / 3, row = e - c * 3;
-      AT[9 + c][rp + 6 + row] = a.jc1[u * 9 + e];
+      AT[9 + c][rp + 6 + row] = p3;
     } else if (lane < 51) {
-      rT[rp + lane - 45] = a.r_dyn[u * 6 + lane - 45];
+      rT[rp + lane - 45] = p3;
     } else if (lane < 54) {
-      rT[rp + 6 + lane - 51] = a.r_cv[u * 3 + lane - 51];
+      rT[rp + 6 + lane - 51] = p3;
     }
   }
-  wave_lds_sync();
-  typedef double d2_t __attribute__((ext_vector_type(2)));
+  wave_order();
+  // [D_l | g_l] = A^T [A | r] and E_l = A_next^T B on the f64 matrix cores
+  // (v_mfma_f64_16x16x4_f64, MI355X_MICROARCH.md / cdna_hip_programming.md fragment maps:
+  // A operand lane l = (i = l & 15, k = l >> 4), B operand (k = l >> 4, j = l & 15),
+  // C/D lane l, register v = (row (l >> 4) + 4 v, col l & 15)).  Rows of the staged
+  // transposes are the k dimension, 4 per instruction; variables 12..15 are zero padding
+  // except B's column 12, which carries r so that C[:, 12] = A^T r = g.
+  typedef double d4_t __attribute__((ext_vector_type(4)));
+  const int li = lane & 15, lk = lane >> 4;
+  d4_t cD = {0.0, 0.0, 0.0, 0.0}, cE = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < RPP / 4; ++q) {
+    const int row = 4 * q + lk;
+    const double at = li < NV ? AT[li][row] : 0.0;
+    const double bv = li < NV ? at : (li == NV ? rT[row] : 0.0);
+    cD = __builtin_amdgcn_mfma_f64_16x16x4f64(at, bv, cD, 0, 0, 0);
+  }
+  if (nxt) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int row = 4 * q + lk;
+      const double an = li < NV ? ANT[li][row] : 0.0;
+      const double bt = li < NV ? BT[li][row] : 0.0;
+      cE = __builtin_amdgcn_mfma_f64_16x16x4f64(an, bt, cE, 0, 0, 0);
+    }
+  }
   double* Dl = a.D + f * NB;
   double* El = nxt ? a.E + ((long)t * npair + l) * NB : nullptr;
   double* gl = a.g + f * NV;
-  for (int w = lane; w < 108; w += 64) {
-    if (w < 96) {  // D (w < 48) or E: row i, columns j0 .. j0 + 2
-      const bool isD = w < 48;
-      if (!isD && !El) continue;
-      const int wi = isD ? w : w - 48;
-      const int i = wi >> 2, j0 = (wi & 3) * 3;
-      double s[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-      if (isD) {
-#pragma unroll 3
-        for (int q = 0; q < RP; q += 2) {
-          const d2_t ai = *reinterpret_cast<const d2_t*>(&AT[i][q]);
 #pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const d2_t aj = *reinterpret_cast<const d2_t*>(&AT[j0 + c][q]);
-            s[c][0] += ai[0] * aj[0];
-            s[c][1] += ai[1] * aj[1];
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const double v = s[c][0] + s[c][1];
-          Dl[i * NV + j0 + c] = v;
-          blk[i * NV + j0 + c] = v;
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 10; q += 2) {
-          const d2_t ai = *reinterpret_cast<const d2_t*>(&ANT[i][q]);
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const d2_t bj = *reinterpret_cast<const d2_t*>(&BT[j0 + c][q]);
-            s[c][0] += ai[0] * bj[0];
-            s[c][1] += ai[1] * bj[1];
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const double v = s[c][0] + s[c][1];
-          El[i * NV + j0 + c] = v;
-          blk[NB + i * NV + j0 + c] = v;
-        }
+  for (int v = 0; v < 4; ++v) {
+    const int i = lk + 4 * v;
+    if (i >= NV) continue;
+    if (li < NV) {
+      Dl[i * NV + li] = cD[v];
+      blk[i * NV + li] = cD[v];
+      if (El) {
+        El[i * NV + li] = cE[v];
+        blk[NB + i * NV + li] = cE[v];
       }
-    } else {  // g[i]
-      const int i = w - 96;
-      double s0 = 0.0, s1 = 0.0;
-#pragma unroll 3
-      for (int q = 0; q < RP; q += 2) {
-        const d2_t ai = *reinterpret_cast<const d2_t*>(&AT[i][q]);
-        const d2_t r = *reinterpret_cast<const d2_t*>(&rT[q]);
-        s0 += ai[0] * r[0];
-        s1 += ai[1] * r[1];
-      }
-      gl[i] = s0 + s1;
-      blk[2 * NB + i] = s0 + s1;
+    } else if (li == NV) {
+      gl[i] = cD[v];
+      blk[2 * NB + i] = cD[v];
     }
   }
 }
@@ -273,7 +310,7 @@ __device__ __forceinline__ double gn_rcp(double x) {
 // hands row k round through LDS (one wave: LDS ops run in order) and uses symmetry for
 // column k.
 template <int RP, int NA, int SOLVER>
-__global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
+__global__ __launch_bounds__(64 * (NA + 1), 3) void gn_step_kernel(GnArgs a) {
   using namespace gn;
   constexpr int BLK = 2 * NB + NV;  // D | E | g of one frame
   constexpr int R = NA + 2;
@@ -306,11 +343,14 @@ __global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
   double* ws = a.ws + (size_t)t * L * GN_WSF;
   int info = 0;
   if constexpr (SOLVER == 1) {
+    // the solver's chain is the launch's critical path: it wins issue arbitration against
+    // the assembler waves of its own and of the CU's other workgroups
+    __builtin_amdgcn_s_setprio(3);
     __shared__ __attribute__((aligned(16))) double bs[NV];
+    __shared__ __attribute__((aligned(16))) double rk2[2 * NV];  // the sweep's pivot rows k, k + 1
     double* Mp = Lp;  // M_{l-1}, row-major
     double* Pb = Wt;  // G_{l-1}
     double* zp = ys;  // z_{l-1}
-    double* rowk = Ld;  // the sweep's current pivot row
     typedef double d2_t __attribute__((ext_vector_type(2)));
     const bool act = i < 36;
     const int ii = act ? i : 35;
@@ -330,18 +370,21 @@ __global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
         double b = -bc[2 * NB + r];
         if (l > 0) {
           // G_{l-1}[r][c0..] = sum_k M_{l-1}[r][k] E_{l-1}[k][c0..]
-          double pv[4] = {0.0, 0.0, 0.0, 0.0};
+          double pv[4] = {0.0, 0.0, 0.0, 0.0}, ph[4] = {0.0, 0.0, 0.0, 0.0};  // even / odd k
 #pragma unroll
           for (int k = 0; k < NV; ++k) {
             const double m = Mp[r * NV + k];
             const d2_t e0 = *reinterpret_cast<const d2_t*>(bp + NB + k * NV + c0);
             const d2_t e1 = *reinterpret_cast<const d2_t*>(bp + NB + k * NV + c0 + 2);
-            pv[0] += m * e0[0];
-            pv[1] += m * e0[1];
-            pv[2] += m * e1[0];
-            pv[3] += m * e1[1];
+            double* acc = (k & 1) ? ph : pv;
+            acc[0] += m * e0[0];
+            acc[1] += m * e0[1];
+            acc[2] += m * e1[0];
+            acc[3] += m * e1[1];
           }
-          wave_lds_sync();  // every lane is past its reads of M_{l-1} / G_{l-2}
+#pragma unroll
+          for (int c = 0; c < 4; ++c) pv[c] += ph[c];
+          wave_order();  // every lane is past its reads of M_{l-1} / G_{l-2}
           if (act) {
             *reinterpret_cast<d2_t*>(Pb + r * NV + c0) = d2_t{pv[0], pv[1]};
             *reinterpret_cast<d2_t*>(Pb + r * NV + c0 + 2) = d2_t{pv[2], pv[3]};
@@ -349,74 +392,89 @@ __global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) gw[c] = pv[c];
           }
-          wave_lds_sync();
+          wave_order();
           // S -= E_{l-1}^T G_{l-1};  b -= E_{l-1}^T z_{l-1}
-          double s2[4] = {0.0, 0.0, 0.0, 0.0}, b2 = 0.0;
+          double s2[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}}, b2[2] = {0.0, 0.0};
 #pragma unroll
           for (int k = 0; k < NV; ++k) {
             const double ek = bp[NB + k * NV + r];
             const d2_t p0 = *reinterpret_cast<const d2_t*>(Pb + k * NV + c0);
             const d2_t p1 = *reinterpret_cast<const d2_t*>(Pb + k * NV + c0 + 2);
-            s2[0] += ek * p0[0];
-            s2[1] += ek * p0[1];
-            s2[2] += ek * p1[0];
-            s2[3] += ek * p1[1];
-            b2 += ek * zp[k];
+            s2[k & 1][0] += ek * p0[0];
+            s2[k & 1][1] += ek * p0[1];
+            s2[k & 1][2] += ek * p1[0];
+            s2[k & 1][3] += ek * p1[1];
+            b2[k & 1] += ek * zp[k];
           }
 #pragma unroll
-          for (int c = 0; c < 4; ++c) sv[c] -= s2[c];
-          b -= b2;
+          for (int c = 0; c < 4; ++c) sv[c] -= s2[0][c] + s2[1][c];
+          b -= b2[0] + b2[1];
         }
         gn_stamp(a, t, 66 + 4 * l);
-        // M_l = S_l^-1: symmetric sweep, pivot k = 0 .. 11 (ends with -S^-1)
+        // M_l = S_l^-1: symmetric sweep with 2 x 2 pivot blocks K = {k, k + 1}, k = 0, 2, .., 10
+        // (ends with -S^-1):  S_KK <- -P^-1,  S_iK <- S_iK P^-1,  S_Kj <- P^-1 S_Kj,
+        // S_ij <- S_ij - S_iK P^-1 S_Kj  (P = S_KK).  P is positive definite iff a > 0 and
+        // det > 0 -- the two scalar pivots a, d - b^2 / a of the Cholesky / LDL^T test.
         bool bad = false;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-          wave_lds_sync();  // previous step's reads of rowk done (program order + compiler fence)
-          if (act && r == k) {
-            *reinterpret_cast<d2_t*>(rowk + c0) = d2_t{sv[0], sv[1]};
-            *reinterpret_cast<d2_t*>(rowk + c0 + 2) = d2_t{sv[2], sv[3]};
+#pragma unroll 1
+        for (int k = 0; k < NV; k += 2) {
+          if (act && (r >> 1) == (k >> 1)) {  // rows k, k + 1 -> the pivot-row buffer
+            double* dst = rk2 + (r - k) * NV + c0;
+            *reinterpret_cast<d2_t*>(dst) = d2_t{sv[0], sv[1]};
+            *reinterpret_cast<d2_t*>(dst + 2) = d2_t{sv[2], sv[3]};
           }
-          wave_lds_sync();
-          double piv = rowk[k];
-          const double ark = rowk[r];  // S[r][k] = S[k][r] (symmetric)
-          const d2_t k0 = *reinterpret_cast<const d2_t*>(rowk + c0);
-          const d2_t k1 = *reinterpret_cast<const d2_t*>(rowk + c0 + 2);
-          const double akj[4] = {k0[0], k0[1], k1[0], k1[1]};
-          if (!(piv > 0.0)) {
+          wave_order();
+          const d2_t pa = *reinterpret_cast<const d2_t*>(rk2 + k);       // S[k][k], S[k][k+1]
+          const double pd = rk2[NV + k + 1];                             // S[k+1][k+1]
+          const double u0 = rk2[r], u1 = rk2[NV + r];                    // S[r][k], S[r][k+1] (symmetric)
+          const d2_t x0 = *reinterpret_cast<const d2_t*>(rk2 + c0);
+          const d2_t x1 = *reinterpret_cast<const d2_t*>(rk2 + c0 + 2);
+          const d2_t y0 = *reinterpret_cast<const d2_t*>(rk2 + NV + c0);
+          const d2_t y1 = *reinterpret_cast<const d2_t*>(rk2 + NV + c0 + 2);
+          const double vk[4] = {x0[0], x0[1], x1[0], x1[1]};   // S[k][c0 ..]
+          const double vk1[4] = {y0[0], y0[1], y1[0], y1[1]};  // S[k+1][c0 ..]
+          double a0 = pa[0], b0 = pa[1], d0 = pd;
+          double det = a0 * d0 - b0 * b0;
+          if (!(a0 > 0.0) || !(det > 0.0)) {
             bad = true;
-            piv = 1.0;
+            a0 = 1.0;
+            b0 = 0.0;
+            d0 = 1.0;
+            det = 1.0;
           }
-          const double ip = gn_rcp(piv);
-          const double f = ark * ip;
+          const double id = gn_rcp(det);
+          const double q00 = d0 * id, q01 = -b0 * id, q11 = a0 * id;  // P^-1 (symmetric)
+          // one formula for every element (branch-free): with (al0, al1) = row r - k of P^-1
+          // for the pivot rows and -(S_rK P^-1) otherwise,
+          //   j not in K:  S'[r][j] = (r in K ? 0 : S[r][j]) + al0 S[k][j] + al1 S[k+1][j]
+          //   j in K:      S'[r][j] = -(j == k ? al0 : al1)
+          const bool rk = (r >> 1) == (k >> 1);
+          const double al0 = rk ? (r == k ? q00 : q01) : -(u0 * q00 + u1 * q01);
+          const double al1 = rk ? (r == k ? q01 : q11) : -(u0 * q01 + u1 * q11);
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int j = c0 + c;
-            if (r == k)
-              sv[c] = j == k ? -ip : akj[c] * ip;
-            else if (j == k)
-              sv[c] = f;
-            else
-              sv[c] -= f * akj[c];
+            const double gen = fma(al0, vk[c], fma(al1, vk1[c], rk ? 0.0 : sv[c]));
+            sv[c] = (j >> 1) == (k >> 1) ? -(j == k ? al0 : al1) : gen;
           }
         }
         if (bad) {
           info = l + 1;  // the solver wave idles through the remaining frames' hand-overs
         } else {
-          wave_lds_sync();
+          wave_order();
           if (act) {
             *reinterpret_cast<d2_t*>(Mp + r * NV + c0) = d2_t{-sv[0], -sv[1]};
             *reinterpret_cast<d2_t*>(Mp + r * NV + c0 + 2) = d2_t{-sv[2], -sv[3]};
             if (c0 == 0) bs[r] = b;
           }
-          wave_lds_sync();
+          wave_order();
           double z0 = 0.0, z1 = 0.0;
 #pragma unroll
           for (int j = 0; j < NV; j += 2) {
             z0 += Mp[r * NV + j] * bs[j];
             z1 += Mp[r * NV + j + 1] * bs[j + 1];
           }
-          wave_lds_sync();
+          wave_order();
           if (act && c0 == 0) {
             zp[r] = z0 + z1;
             wl[NB + r] = z0 + z1;
@@ -428,37 +486,45 @@ __global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
     }
     gn_stamp(a, t, 250);
     if (!info) {
-      // backward: delta_l = z_l - G_l delta_{l+1}; lane i < 12: row i
+      // backward: delta_l = z_l - G_l delta_{l+1}; lane i < 12: row i.  G rows and z are
+      // read from the workspace two frames ahead (a ring of three register sets), so the
+      // chain waits on the LDS broadcast of delta only, not on memory
       const int ir = i < NV ? i : NV - 1;
       double* dl = bs;  // delta_{l+1}
-      double G_n[NV], z_n = ws[(size_t)(L - 1) * GN_WSF + NB + ir];
+      double Gq[3][NV], zq[3];
+      auto ld = [&](int l, int slot) __attribute__((always_inline)) {
+        const double* wn = ws + (size_t)l * GN_WSF;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) Gq[slot][k] = wn[ir * NV + k];
+        zq[slot] = wn[NB + ir];
+      };
+      ld(L - 1, (L - 1) % 3);
+      if (L >= 2) ld(L - 2, (L - 2) % 3);
       for (int l = L - 1; l >= 0; --l) {
-        double Gr[NV];
-#pragma unroll
-        for (int k = 0; k < NV; ++k) Gr[k] = G_n[k];
-        const double z = z_n;
-        if (l > 0) {  // frame l - 1's G row and z, one frame ahead
-          const double* wn = ws + (size_t)(l - 1) * GN_WSF;
-#pragma unroll
-          for (int k = 0; k < NV; ++k) G_n[k] = wn[ir * NV + k];
-          z_n = wn[NB + ir];
-        }
-        double d = z;
-        if (l + 1 < L) {
-          double d0 = 0.0, d1 = 0.0;
-#pragma unroll
-          for (int k = 0; k < NV; k += 2) {
-            d0 += Gr[k] * dl[k];
-            d1 += Gr[k + 1] * dl[k + 1];
-          }
-          d -= d0 + d1;
-        }
-        wave_lds_sync();
+        if (l >= 2) ld(l - 2, (l - 2) % 3);
+        double d = 0.0;
+        // the ring slot is l % 3: a runtime index, so select it with three compile-time branches
+#define GN_BWD(S)                                              \
+  {                                                            \
+    d = zq[S];                                                 \
+    if (l + 1 < L) {                                           \
+      double d0 = 0.0, d1 = 0.0;                               \
+      _Pragma("unroll") for (int k = 0; k < NV; k += 2) {      \
+        d0 += Gq[S][k] * dl[k];                                \
+        d1 += Gq[S][k + 1] * dl[k + 1];                        \
+      }                                                        \
+      d -= d0 + d1;                                            \
+    }                                                          \
+  }
+        const int sl = l % 3;
+        if (sl == 0) GN_BWD(0) else if (sl == 1) GN_BWD(1) else GN_BWD(2)
+#undef GN_BWD
+        wave_order();
         if (i < NV) {
           dl[i] = d;
           a.delta[((size_t)t * L + l) * NV + i] = d;
         }
-        wave_lds_sync();
+        wave_order();
       }
     } else {
       for (int e = i; e < L * NV; e += 64) a.delta[(size_t)t * L * NV + e] = NAN;
@@ -626,7 +692,7 @@ __global__ __launch_bounds__(64 * (NA + 1)) void gn_step_kernel(GnArgs a) {
   if (a.info && i == 0) a.info[t] = info;
 }
 
-// assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * solver;
+// assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * legacy;
 // 0 = the shipped choice)
 static int g_gn_na = 0;
 static unsigned long long* g_gn_trace = nullptr;
@@ -641,12 +707,14 @@ static void launch_gn_sv(const GnArgs& a, int na, hipStream_t s) {
   }
 }
 
+// shipped: solver 1 (swept inverses, round 3: 1000 x 24 152 -> 90 us, 3 x 24 123 -> 70 us
+// with the MFMA assembly and batched loads); v & 8 selects the round-2 block Cholesky
 template <int RP>
 static void launch_gn(const GnArgs& a, int v, hipStream_t s) {
   if (v & 8)
-    launch_gn_sv<RP, 1>(a, v & 7, s);
-  else
     launch_gn_sv<RP, 0>(a, v & 7, s);
+  else
+    launch_gn_sv<RP, 1>(a, v & 7, s);
 }
 
 }  // namespace pa
@@ -659,7 +727,7 @@ int pa_debug_gn_set_trace(unsigned long long* trace_dev) {
 }
 
 int pa_debug_gn_set_assemblers(int na) {
-  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 16, "gn variant %d: assembler waves (0..4) + 8 * solver (0, 1)", na);
+  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 16, "gn variant %d: assembler waves (0..4) + 8 * legacy solver", na);
   pa::g_gn_na = na;
   return PA_OK;
 }

@@ -91,10 +91,21 @@ def test_pose_tick_chain_vs_oracle(model):
     # 3. the GN step on the device's own whitened factors
     f = {k: lin[k].cpu().numpy() for k in ("r_proj", "j_proj", "status", "r_dyn", "j_dyn0", "j_dyn1", "j_dyn2",
                                            "j_dyn3", "r_cv", "j_cv0", "j_cv1")}
-    _, _, d = G.gn_step(f, n, LW, nk, SIG["lam"])
+    H, g, d = G.gn_step(f, n, LW, nk, SIG["lam"])
     dd = p.gn.out["delta"].cpu().numpy()
     assert (info == 0).all()
-    np.testing.assert_allclose(dd.reshape(n, -1), d, rtol=1e-7, atol=1e-9 * np.abs(d).max())
+    # a solver is judged by its backward error (the damped normal equations' residual) and
+    # by a forward error within the conditioning bound; this window's system is far worse
+    # conditioned than tests/test_gn_gpu.py's (40 px pixel sigma against 0.1 dynamics
+    # sigmas), so the forward tolerance scales with cond(H + lam I)
+    eps = np.finfo(np.float64).eps
+    for t in range(n):
+        M = H[t] + SIG["lam"] * np.eye(H.shape[1])
+        x = dd.reshape(n, -1)[t]
+        res = M @ x + g[t]
+        assert np.abs(res).max() <= 1e-11 * (np.abs(M).max() * np.abs(x).max() + np.abs(g[t]).max()), t
+        bound = 10 * np.linalg.cond(M) * eps * np.abs(d[t]).max()
+        np.testing.assert_allclose(x, d[t], rtol=0, atol=max(bound, 1e-9 * np.abs(d[t]).max()))
     # 4. retract of the advanced window by the device's delta = the window the tick left
     ret = F.window_retract(adv, dd, info)
     for k in ("pose", "vel", "angvel"):

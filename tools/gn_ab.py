@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--na", type=int, nargs="+", default=[0, 3, 4, 8, 10, 11, 12])
+    p.add_argument("--na", type=int, nargs="+", default=[8, 0, 3])
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=20)
     a = p.parse_args()
@@ -63,7 +63,7 @@ if __name__ == "__main__" and not os.environ.get("GN_TRACE"):
     main()
 
 
-def trace(T=3, L=24, variant=8):
+def trace(T=3, L=24, variant=0):
     """Per-frame stamps of one traced pa_trajectory_gn_step (pa_debug_gn_set_trace)."""
     import numpy as np
     import torch
@@ -99,4 +99,4 @@ def trace(T=3, L=24, variant=8):
 
 
 if __name__ == "__main__" and os.environ.get("GN_TRACE"):
-    trace()
+    trace(T=int(os.environ.get("GN_TRACE_T", "3")), variant=int(os.environ.get("GN_VARIANT", "0")))
