@@ -225,7 +225,8 @@ __device__ __forceinline__ void gx_head(const ConvArgs& a, char* smem, const f32
 }
 
 // DBG (timing experiments only, wrong results): 1 = no waits / barriers in the K loop,
-// 2 = also no weight / patch DMAs in the K loop, 3 = no K loop (prologue + epilogue);
+// 2 = also no weight / patch DMAs in the K loop, 3 = no K loop (prologue + epilogue),
+// 5 = DMAs and barriers but no vmcnt waits, 6 = barriers only (no DMAs in the K loop);
 // 4 = the shipped kernel plus s_memrealtime stamps into a.trace (conv.h trace_stamp)
 // FD: fragment reads run FD half-steps ahead of the MFMAs (FD + 1 register sets)
 // X3 virtual block vb of a CIN = 64 * NCB conv: the 64-channel block of the activation
@@ -462,8 +463,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     if constexpr (S + 1 < NSTEPS) read_frags(xic<2 * S + 1 + FD>{});
     // DMAs after this step's LDS reads (they are issued by then; see xdma16)
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (S + PD < NSTEPS && DBG < 2) dma_w(S + PD);
-    if constexpr (CB + 1 < VB::NVB && S == plan.ps(CB + 1) && DBG < 2) dma_patch(CB + 1, (CB + 1) & 1);
+    if constexpr (S + PD < NSTEPS && (DBG < 2 || DBG == 5)) dma_w(S + PD);
+    if constexpr (CB + 1 < VB::NVB && S == plan.ps(CB + 1) && (DBG < 2 || DBG == 5)) dma_patch(CB + 1, (CB + 1) & 1);
     if constexpr (S == plan.rs) {
       // vm_after() counts these after this step's DMAs: keep the scheduler from
       // moving the (read-only) loads across them
@@ -474,11 +475,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     __builtin_amdgcn_s_setprio(1);
     mfma(xic<2 * S + 1>{});
     __builtin_amdgcn_s_setprio(0);
-    if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS && (DBG == 0 || DBG == 4)) {
+    if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS && (DBG == 0 || DBG == 4 || DBG == 5 || DBG == 6)) {
       // the next group (steps s+1 .. s+G) reads the fragments of steps up to s+G+1
       // (first half): those weight tiles and their blocks' patches must have landed
       constexpr int V = S + G + 1 < NSTEPS ? S + G + 1 : NSTEPS - 1;
-      xwait_vm<plan.vm_after(S, V)>();
+      if constexpr (DBG != 5) xwait_vm<plan.vm_after(S, V)>();
       __builtin_amdgcn_s_barrier();
     }
   });

@@ -414,8 +414,8 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
   if constexpr (std::is_same<T, _Float16>::value) {
     const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : 4;
     // layers 2-4: conv_gx (deep-ring LDS-DMA, inline-asm DMA, fully unrolled);
-    // variants 50-59 pick its alternatives
-    if (layer >= 2 && (g_variant[layer] == 0 || (g_variant[layer] >= 50 && g_variant[layer] <= 59))) {
+    // variants 50-69 pick its alternatives
+    if (layer >= 2 && (g_variant[layer] == 0 || (g_variant[layer] >= 50 && g_variant[layer] <= 69))) {
       static const char* names[5] = {"", "conv3x3x_l1", "conv3x3x_l2", "conv3x3x_l3", "conv3x3x_l4"};
       if (kname) *kname = (a.epi & EPI_HEAD) ? "conv3x3x_l4_avgpool_fc" : names[layer];
       const int v = g_variant[layer] == 0 ? 0 : g_variant[layer] - 50;

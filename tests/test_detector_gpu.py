@@ -314,3 +314,19 @@ def test_fused_head_repeats_and_batch_changes():
             m.set_variants({})
         for y in ys:
             assert torch.equal(y, ref), B
+
+
+@pytest.mark.parametrize("precision", ["fp32", "fp16"])
+def test_reserve_is_clamped_to_one_chunk(precision):
+    """pa_detector_reserve clamps to the 1,024-frame chunk the forward runs in: reserving a
+    configs[2]-sized batch (24,000 frames; unclamped ~176 GB of f32 workspace) succeeds, and
+    a 4,100-frame forward (five chunks) then matches the same frames forwarded alone."""
+    m = KeypointCNN(num_channels=4, precision=precision)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
+    m.reserve(24000)
+    x = torch.from_numpy(synth.synthetic_frames(0, 8)).cuda()
+    xs = x.repeat(513, 1, 1, 1)[:4100].contiguous()
+    y = m(xs)
+    ref = m(x)
+    for off in (0, 1024, 2048, 4096):
+        assert torch.equal(y[off:off + 4], ref[(off % 8):(off % 8) + 4]), off
