@@ -94,10 +94,12 @@ struct GxPlan {
   int spb = 9;     // steps per 64-channel block (9 taps; conv_s2x.h adds the downsample)
   int spt = 0;     // multi-tile workgroups (conv_s2x.h TPW > 1): steps per tile; the
   int nstore = 0;  // previous tile's `nstore` output stores open every tile's first step
+  int xm = 0;      // X3 merged steps (conv_gx.h XM): the steps of even blocks carry two weight tiles
   // the patch of block c >= 1 is DMA'd at the first group start inside block c - 1
   constexpr int ps(int c) const { return (spb * (c - 1) + g - 1) / g * g; }
   constexpr int ns(int t) const { return (spt && t > 0 && t % spt == 0) ? nstore : 0; }
-  constexpr int nw(int t) const { return t + pd < nsteps ? wdma : 0; }
+  constexpr int wc(int s) const { return (xm && (s / spb) % 2 == 0) ? 2 : 1; }
+  constexpr int nw(int t) const { return t + pd < nsteps ? wdma * wc(t + pd) : 0; }
   constexpr int np(int t) const { return (t / spb + 1 < ncb && t == ps(t / spb + 1)) ? pdma : 0; }
   constexpr int nr(int t) const { return t == rs ? rl : 0; }
   constexpr int cum(int t) const {  // VMEM ops issued in steps 0..t (prologue excluded: it is drained)
@@ -230,12 +232,21 @@ __device__ __forceinline__ void gx_head(const ConvArgs& a, char* smem, const f32
 // 4 = the shipped kernel plus s_memrealtime stamps into a.trace (conv.h trace_stamp)
 // FD: fragment reads run FD half-steps ahead of the MFMAs (FD + 1 register sets)
 // X3 virtual block vb of a CIN = 64 * NCB conv: the 64-channel block of the activation
-// planes [hi | lo] (pblk) and of the weight planes (wblk) it multiplies
-template <bool X3, int NCB>
+// planes [hi | lo] (pblk) and of the weight planes (wblk) it multiplies.
+// XM (merged): 2 virtual blocks per 64-channel block b, (x_hi; w_hi, w_lo) then
+// (x_lo; w_hi): the steps of the first carry two weight tiles (wblk, wblk2) against
+// the same patch fragments, so x_hi is staged and read once for both of its products
+// (LDS fragment reads per MFMA: layer3's 64 x 32 wave tile 0.58 instead of 0.75;
+// barriers per MFMA: 18 steps per block instead of 27).
+template <bool X3, int NCB, bool XM = false>
 struct GxBlocks {
-  static constexpr int NVB = X3 ? 3 * NCB : NCB;
-  static constexpr int pblk(int vb) { return X3 ? (vb % 3 == 2 ? NCB + vb / 3 : vb / 3) : vb; }
-  static constexpr int wblk(int vb) { return X3 ? (vb % 3 == 1 ? NCB + vb / 3 : vb / 3) : vb; }
+  static constexpr int NVB = X3 ? (XM ? 2 : 3) * NCB : NCB;
+  static constexpr int pblk(int vb) {
+    return X3 ? (XM ? (vb % 2 ? NCB + vb / 2 : vb / 2) : (vb % 3 == 2 ? NCB + vb / 3 : vb / 3)) : vb;
+  }
+  static constexpr int wblk(int vb) { return X3 ? (XM ? vb / 2 : (vb % 3 == 1 ? NCB + vb / 3 : vb / 3)) : vb; }
+  static constexpr bool two(int vb) { return XM && vb % 2 == 0; }  // second weight tile: w_lo of block vb / 2
+  static constexpr int wblk2(int vb) { return NCB + vb / 2; }
 };
 
 // hi / lo fp16 pair of an f32 value (hi + lo == v to 2^-22 relative)
@@ -248,11 +259,12 @@ __device__ __forceinline__ HiLo split_x3(float v) {
 }
 
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1,
-          bool WT = true, bool X3 = false>
+          bool WT = true, bool X3 = false, bool XM = false>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
-  using VB = GxBlocks<X3, NCB>;
+  static_assert(!XM || (X3 && FD == 1), "merged X3 steps: fp16x3, fragments half a step ahead");
+  using VB = GxBlocks<X3, NCB, XM>;
   constexpr int XS = X3 ? 2 : 1;  // fp16 planes per activation / weight element
   constexpr int NSTEPS = VB::NVB * 9;
   constexpr int KW = XS * CIN;  // weight elements per tap
@@ -280,8 +292,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   // epilogue loads (bias, residual) issued RSD steps before the end: early enough to
   // land, late enough not to hold their VGPRs across the whole K loop
   constexpr int RSD = 4;
-  constexpr GxPlan plan{NSTEPS, VB::NVB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G};
-  __shared__ __attribute__((aligned(1024))) char smem[2 * PATCHB + NSLOT * WB];
+  constexpr GxPlan plan{NSTEPS, VB::NVB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, 9, 0, 0, XM ? 1 : 0};
+  constexpr int WSLOT = (XM ? 2 : 1) * WB;  // ring slot: one weight tile, or two (XM)
+  static_assert(2 * PATCHB + NSLOT * WSLOT <= 163840, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * PATCHB + NSLOT * WSLOT];
   char* patch = smem;
   char* wring = smem + 2 * PATCHB;
 
@@ -349,7 +363,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     const int vb = s / 9, tap = s % 9;
 #pragma unroll
     for (int i = 0; i < WDMA; ++i)
-      xdma16(wsrc[i] + tap * KW + VB::wblk(vb) * 64, wring + (s % NSLOT) * WB + (i * NW + wid) * 1024);
+      xdma16(wsrc[i] + tap * KW + VB::wblk(vb) * 64, wring + (s % NSLOT) * WSLOT + (i * NW + wid) * 1024);
+    if (VB::two(vb))  // compile-time after inlining (s is a step constant)
+#pragma unroll
+      for (int i = 0; i < WDMA; ++i)
+        xdma16(wsrc[i] + tap * KW + VB::wblk2(vb) * 64, wring + (s % NSLOT) * WSLOT + WB + (i * NW + wid) * 1024);
   };
 
   const int o = xfrag(r16);
@@ -427,26 +445,41 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   static_assert(FD == 1 || FD == 2, "fragment distance");
   constexpr int NSET = FD + 1;
   xu4 fa[NSET][TN], fb[NSET][TM];
+  xu4 fa2[XM ? NSET : 1][XM ? TN : 1];  // XM: the second weight tile's fragments
   auto read_frags = [&](auto kc) __attribute__((always_inline)) {
     constexpr int K = decltype(kc)::value;
     constexpr int S = K >> 1, HG = K & 1, CB = S / 9, TAP = S % 9, SET = K % NSET;
     constexpr int TOFF = (TAP / 3) * PW + (TAP % 3);
     const char* pb = patch + (CB & 1) * PATCHB;
-    const char* wb = wring + (S % NSLOT) * WB;
+    const char* wb = wring + (S % NSLOT) * WSLOT;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
       fa[SET][tn] = *reinterpret_cast<const xu4*>(wb + xswz(wn * WTN + tn * 16 + r16, HG * 4 + q));
+    if constexpr (VB::two(CB))
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        fa2[SET][tn] = *reinterpret_cast<const xu4*>(wb + WB + xswz(wn * WTN + tn * 16 + r16, HG * 4 + q));
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) fb[SET][tm] = *reinterpret_cast<const xu4*>(pb + xswz(ppix[tm] + TOFF, HG * 4 + q));
   };
   auto mfma = [&](auto kc) __attribute__((always_inline)) {
-    constexpr int SET = decltype(kc)::value % NSET;
+    constexpr int K = decltype(kc)::value;
+    constexpr int SET = K % NSET;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
         acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[SET][tn]),
                                                              __builtin_bit_cast(half8, fb[SET][tm]), acc[tm][tn], 0, 0, 0);
+    // XM: x_hi w_lo after every x_hi w_hi of the half-step (TM x TN independent
+    // accumulators between two uses of one)
+    if constexpr (VB::two((K >> 1) / 9))
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa2[SET][tn]),
+                                                               __builtin_bit_cast(half8, fb[SET][tm]), acc[tm][tn], 0, 0, 0);
   };
   // step s + 1's data landed before the barrier that closed step s - 1, so with
   // FD = 2 both its halves are read during step s
@@ -524,7 +557,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
 }
 
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1,
-          bool WT = true, bool X3 = false>
+          bool WT = true, bool X3 = false, bool XM = false>
 static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES) || a.epi == (EPI_RELU | EPI_RES | EPI_HEAD),
            "gx conv: epilogue %d", a.epi);
@@ -548,10 +581,10 @@ static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
       PA_CHECK(false, "gx conv: fused head needs the 2 x 8x8 x 64-channel tile");
     }
   } else if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT, X3>),
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT, X3, XM>),
                        dim3(tiles), dim3(WM * WN * 64), 0, s, a, x);
   else
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT, X3>), dim3(tiles),
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT, X3, XM>), dim3(tiles),
                        dim3(WM * WN * 64), 0, s, a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;

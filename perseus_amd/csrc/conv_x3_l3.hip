@@ -7,7 +7,9 @@ namespace pa {
 int launch_conv3x3_x3_l3(const ConvArgs& a, hipStream_t s) {
   if (a.B <= 0) return PA_OK;
   PA_CHECK(a.Hout == 16 && a.Wout == 16, "x3 conv layer3: %dx%d", a.Hout, a.Wout);
-  return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 0, 1, true, true>(a, true, s);
+  // merged x_hi steps (conv_gx.h XM) shipped; variant 70 keeps three virtual blocks per 64 channels
+  if (g_variant[3] == 70) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 0, 1, true, true>(a, true, s);
+  return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 0, 1, true, true, true>(a, true, s);
 }
 
 }  // namespace pa

@@ -79,46 +79,49 @@ static __device__ int32_t gn_zero_i32[1];  // status source when no status array
 
 // Assembles frame f (of trajectory t, frame index l) with one wave: D_l, E_l (if l + 1 < L)
 // and g_l to the outputs a.D / a.E / a.g and to the LDS block `blk` (D | E | g).
+// The per-lane values of one frame's factors (gn_load_frame), fetched before any is used.
 template <int RP>
-__device__ __forceinline__ void gn_assemble_frame(const GnArgs& a, long f, GnStage<RP>& st, double* blk) {
-  using namespace gn;
-  constexpr int RPP = GnStage<RP>::RPP;
-  double(&AT)[NV][RPP] = st.AT;
-  double(&rT)[RPP] = st.rT;
-  double(&ANT)[NV][12] = st.ANT;
-  double(&BT)[NV][12] = st.BT;
+struct GnFrameLoads {
+  static constexpr int KM = (RP - 18) / 2;        // keypoints this instantiation holds
+  static constexpr int JR = (KM * 12 + 63) / 64;  // projection Jacobian entries per lane
+  double jv[JR];
+  int js[JR];
+  double rv;
+  int rs;
+  double n0, n3, n1, n2, p3;
+};
+
+// Loads of frame f: every value is fetched from an address clamped to a valid element, then
+// selected -- one memory latency per frame (branches around guarded loads made the compiler
+// wait out each load in turn: ~10 round trips).  Nothing loaded decides a branch here, so a
+// caller can issue the next frame's loads before building the current one.
+template <int RP>
+__device__ __forceinline__ void gn_load_frame(const GnArgs& a, long f, GnFrameLoads<RP>& ld) {
+  constexpr int JR = GnFrameLoads<RP>::JR;
   const int lane = threadIdx.x & 63;
   const int t = (int)(f / a.L), l = (int)(f - (long)t * a.L);
   const int npair = a.L - 1;
   const int K = a.K;
   const bool nxt = l + 1 < a.L, prv = l > 0;
-  // ---- loads: every value of the frame is fetched before any is used, from addresses
-  // clamped to valid elements, then selected -- one memory latency per frame (branches
-  // around guarded loads made the compiler wait out each load in turn: ~10 round trips)
-  constexpr int KM = (RP - 18) / 2;        // keypoints this instantiation holds
-  constexpr int JR = (KM * 12 + 63) / 64;  // projection Jacobian entries per lane
   const long fk = f * K;
-  // (the status pointer test is uniform; no loaded value decides a branch before the
-  // last load is issued)
+  // (the status pointer test is uniform)
   const bool has_st = a.st_proj != nullptr;
   const int32_t* stp = has_st ? a.st_proj : gn_zero_i32;  // always a valid address
-  double jv[JR];
-  int js[JR];
 #pragma unroll
   for (int q = 0; q < JR; ++q) {
     const int e = lane + 64 * q;
     const bool v = e < K * 12;
     const long u = fk + (v ? e / 12 : 0);
-    jv[q] = a.j_proj[v ? fk * 12 + e : fk * 12];  // (u, c, row) = (e / 12, (e % 12) / 2, e & 1)
-    js[q] = stp[has_st ? u : 0];
+    ld.jv[q] = a.j_proj[v ? fk * 12 + e : fk * 12];  // (u, c, row) = (e / 12, (e % 12) / 2, e & 1)
+    ld.js[q] = stp[has_st ? u : 0];
   }
   const bool vr = lane < 2 * K;
   const long ur = fk + (vr ? lane >> 1 : 0);
-  const double rv = a.r_proj[vr ? fk * 2 + lane : fk * 2];
-  const int rs = stp[has_st ? ur : 0];
+  ld.rv = a.r_proj[vr ? fk * 2 + lane : fk * 2];
+  ld.rs = stp[has_st ? ur : 0];
   // pair factors: lane classes [0, 36) dynamics J (6 x 6 column-major; < 18 also the 6 x 3
   // J1 / J2), [36, 45) constant velocity (3 x 3), [45, 51) dynamics r, [51, 54) const-vel r
-  double n0 = 0.0, n3 = 0.0, n1 = 0.0, n2 = 0.0, p3 = 0.0;
+  ld.n0 = ld.n3 = ld.n1 = ld.n2 = ld.p3 = 0.0;
   if (npair > 0) {
     const long un = (long)t * npair + (nxt ? l : 0), up = (long)t * npair + (prv ? l - 1 : 0);
     const int e36 = lane < 36 ? lane : 0, e9 = lane >= 36 && lane < 45 ? lane - 36 : 0;
@@ -131,12 +134,45 @@ __device__ __forceinline__ void gn_assemble_frame(const GnArgs& a, long f, GnSta
     const double* sp = cls == 0 ? a.j3 + up * 36 + e36 : cls == 1 ? a.jc1 + up * 9 + e9
                      : cls == 2 ? a.r_dyn + up * 6 + e6 : cls == 3 ? a.r_cv + up * 3 + e3 : a.j3;
     const int e18 = lane < 18 ? lane : 0;
-    n0 = *sa;
-    n3 = *sb;
-    p3 = *sp;
-    n1 = a.j1[un * 18 + e18];
-    n2 = a.j2[un * 18 + e18];
+    ld.n0 = *sa;
+    ld.n3 = *sb;
+    ld.p3 = *sp;
+    ld.n1 = a.j1[un * 18 + e18];
+    ld.n2 = a.j2[un * 18 + e18];
   }
+}
+
+template <int RP>
+__device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const GnFrameLoads<RP>& ld, GnStage<RP>& st,
+                                               double* blk);
+
+template <int RP>
+__device__ __forceinline__ void gn_assemble_frame(const GnArgs& a, long f, GnStage<RP>& st, double* blk) {
+  GnFrameLoads<RP> ld;
+  gn_load_frame<RP>(a, f, ld);
+  gn_build_frame<RP>(a, f, ld, st, blk);
+}
+
+template <int RP>
+__device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const GnFrameLoads<RP>& ld, GnStage<RP>& st,
+                                               double* blk) {
+  using namespace gn;
+  constexpr int RPP = GnStage<RP>::RPP;
+  constexpr int JR = GnFrameLoads<RP>::JR;
+  double(&AT)[NV][RPP] = st.AT;
+  double(&rT)[RPP] = st.rT;
+  double(&ANT)[NV][12] = st.ANT;
+  double(&BT)[NV][12] = st.BT;
+  const int lane = threadIdx.x & 63;
+  const int t = (int)(f / a.L), l = (int)(f - (long)t * a.L);
+  const int npair = a.L - 1;
+  const int K = a.K;
+  const bool nxt = l + 1 < a.L, prv = l > 0;
+  const bool vr = lane < 2 * K;
+  const double(&jv)[JR] = ld.jv;
+  const int(&js)[JR] = ld.js;
+  const double rv = ld.rv, n0 = ld.n0, n3 = ld.n3, n1 = ld.n1, n2 = ld.n2, p3 = ld.p3;
+  const int rs = ld.rs;
   // ---- staging: zero, then fill (one wave: its LDS ops run in order)
   for (int e = lane; e < NV * RPP; e += 64) (&AT[0][0])[e] = 0.0;
   for (int e = lane; e < NV * 12; e += 64) {
@@ -298,6 +334,207 @@ __device__ __forceinline__ double gn_rcp(double x) {
   return y;
 }
 
+typedef double gn_d2 __attribute__((ext_vector_type(2)));
+#ifndef GN_CU
+#define GN_CU 3  // k-pair unroll of gn_couple's loops (6 = fully unrolled)
+#endif
+
+// One eliminated frame's state in LDS (a solver wave's own): M = S^-1 (row-major), G =
+// M E' (the S update reads it across lanes), z, this frame's b, the sweep's pivot rows.
+struct GnChainLds {
+  double M[gn::NB];
+  double G[gn::NB];
+  double z[gn::NV];
+  double bs[gn::NV];
+  double rk2[2 * gn::NV];
+};
+
+// (sv, b) -= the coupling to the previously eliminated frame (lane: row r, columns c0 .. c0 + 3):
+//   G = Mprev E',   sv -= E'^T G,   b -= E'^T zprev,
+// with E'(k, c) = eb[k * NV + c] (MIR = false: E_{l-1}, from the previous frame's slot) or
+// eb[c * NV + k] (MIR = true: the current frame's own E_l, transposed -- the bottom-up chain).
+// G goes to Gout (LDS) and, when gws is given, to the workspace (row-major, back substitution).
+template <bool MIR>
+__device__ __forceinline__ void gn_couple(const double* Mprev, const double* zprev, const double* eb, double* Gout,
+                                          double* gws, int r, int c0, bool act, double (&sv)[4], double& b) {
+  using namespace gn;
+  double pv[4] = {0.0, 0.0, 0.0, 0.0}, ph[4] = {0.0, 0.0, 0.0, 0.0};  // even / odd k
+  // k in pairs, the pair loop unrolled by NU only: fully unrolled, the compiler hoists all
+  // 60 LDS reads and the 4-wave workgroup's 128-VGPR budget spills
+#pragma unroll GN_CU
+  for (int k2 = 0; k2 < NV; k2 += 2) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = k2 + h;
+      const double m = Mprev[r * NV + k];
+      double e[4];
+      if constexpr (MIR) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) e[c] = eb[(c0 + c) * NV + k];
+      } else {
+        const gn_d2 e0 = *reinterpret_cast<const gn_d2*>(eb + k * NV + c0);
+        const gn_d2 e1 = *reinterpret_cast<const gn_d2*>(eb + k * NV + c0 + 2);
+        e[0] = e0[0];
+        e[1] = e0[1];
+        e[2] = e1[0];
+        e[3] = e1[1];
+      }
+      double* acc = h ? ph : pv;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] += m * e[c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) pv[c] += ph[c];
+  wave_order();  // every lane is past its reads of Gout's previous contents
+  if (act) {
+    *reinterpret_cast<gn_d2*>(Gout + r * NV + c0) = gn_d2{pv[0], pv[1]};
+    *reinterpret_cast<gn_d2*>(Gout + r * NV + c0 + 2) = gn_d2{pv[2], pv[3]};
+    if (gws)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) gws[r * NV + c0 + c] = pv[c];
+  }
+  wave_order();
+  double s2[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}}, b2[2] = {0.0, 0.0};
+#pragma unroll GN_CU
+  for (int k2 = 0; k2 < NV; k2 += 2) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = k2 + h;
+      const double ek = MIR ? eb[r * NV + k] : eb[k * NV + r];
+      const gn_d2 p0 = *reinterpret_cast<const gn_d2*>(Gout + k * NV + c0);
+      const gn_d2 p1 = *reinterpret_cast<const gn_d2*>(Gout + k * NV + c0 + 2);
+      s2[h][0] += ek * p0[0];
+      s2[h][1] += ek * p0[1];
+      s2[h][2] += ek * p1[0];
+      s2[h][3] += ek * p1[1];
+      b2[h] += ek * zprev[k];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) sv[c] -= s2[0][c] + s2[1][c];
+  b -= b2[0] + b2[1];
+}
+
+// M = S^-1 by the symmetric sweep operator with 2 x 2 pivot blocks K = {k, k + 1}, k = 0, 2, .., 10
+// (ends with -S^-1):  S_KK <- -P^-1,  S_iK <- S_iK P^-1,  S_Kj <- P^-1 S_Kj,
+// S_ij <- S_ij - S_iK P^-1 S_Kj  (P = S_KK).  P is positive definite iff a > 0 and
+// det > 0 -- the two scalar pivots a, d - b^2 / a of the Cholesky / LDL^T test.  Returns
+// false on a pivot block that is not positive definite; otherwise sv is row r of -M.
+__device__ __forceinline__ bool gn_sweep(double (&sv)[4], double* rk2, int r, int c0, bool act) {
+  using namespace gn;
+  bool bad = false;
+#pragma unroll 1
+  for (int k = 0; k < NV; k += 2) {
+    if (act && (r >> 1) == (k >> 1)) {  // rows k, k + 1 -> the pivot-row buffer
+      double* dst = rk2 + (r - k) * NV + c0;
+      *reinterpret_cast<gn_d2*>(dst) = gn_d2{sv[0], sv[1]};
+      *reinterpret_cast<gn_d2*>(dst + 2) = gn_d2{sv[2], sv[3]};
+    }
+    wave_order();
+    const gn_d2 pa = *reinterpret_cast<const gn_d2*>(rk2 + k);  // S[k][k], S[k][k+1]
+    const double pd = rk2[NV + k + 1];                          // S[k+1][k+1]
+    const double u0 = rk2[r], u1 = rk2[NV + r];                 // S[r][k], S[r][k+1] (symmetric)
+    const gn_d2 x0 = *reinterpret_cast<const gn_d2*>(rk2 + c0);
+    const gn_d2 x1 = *reinterpret_cast<const gn_d2*>(rk2 + c0 + 2);
+    const gn_d2 y0 = *reinterpret_cast<const gn_d2*>(rk2 + NV + c0);
+    const gn_d2 y1 = *reinterpret_cast<const gn_d2*>(rk2 + NV + c0 + 2);
+    const double vk[4] = {x0[0], x0[1], x1[0], x1[1]};   // S[k][c0 ..]
+    const double vk1[4] = {y0[0], y0[1], y1[0], y1[1]};  // S[k+1][c0 ..]
+    double a0 = pa[0], b0 = pa[1], d0 = pd;
+    double det = a0 * d0 - b0 * b0;
+    if (!(a0 > 0.0) || !(det > 0.0)) {
+      bad = true;
+      a0 = 1.0;
+      b0 = 0.0;
+      d0 = 1.0;
+      det = 1.0;
+    }
+    const double id = gn_rcp(det);
+    const double q00 = d0 * id, q01 = -b0 * id, q11 = a0 * id;  // P^-1 (symmetric)
+    // one formula for every element (branch-free): with (al0, al1) = row r - k of P^-1
+    // for the pivot rows and -(S_rK P^-1) otherwise,
+    //   j not in K:  S'[r][j] = (r in K ? 0 : S[r][j]) + al0 S[k][j] + al1 S[k+1][j]
+    //   j in K:      S'[r][j] = -(j == k ? al0 : al1)
+    const bool rk = (r >> 1) == (k >> 1);
+    const double al0 = rk ? (r == k ? q00 : q01) : -(u0 * q00 + u1 * q01);
+    const double al1 = rk ? (r == k ? q01 : q11) : -(u0 * q01 + u1 * q11);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int j = c0 + c;
+      const double gen = fma(al0, vk[c], fma(al1, vk1[c], rk ? 0.0 : sv[c]));
+      sv[c] = (j >> 1) == (k >> 1) ? -(j == k ? al0 : al1) : gen;
+    }
+  }
+  return !bad;
+}
+
+// after a successful sweep: M (= -sv) and b to LDS, z = M b (returned on every lane for its row r)
+__device__ __forceinline__ double gn_finish(const double (&sv)[4], double b, GnChainLds& C, int r, int c0, bool act) {
+  using namespace gn;
+  wave_order();
+  if (act) {
+    *reinterpret_cast<gn_d2*>(C.M + r * NV + c0) = gn_d2{-sv[0], -sv[1]};
+    *reinterpret_cast<gn_d2*>(C.M + r * NV + c0 + 2) = gn_d2{-sv[2], -sv[3]};
+    if (c0 == 0) C.bs[r] = b;
+  }
+  wave_order();
+  double z0 = 0.0, z1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NV; j += 2) {
+    z0 += C.M[r * NV + j] * C.bs[j];
+    z1 += C.M[r * NV + j + 1] * C.bs[j + 1];
+  }
+  wave_order();
+  if (act && c0 == 0) C.z[r] = z0 + z1;
+  return z0 + z1;
+}
+
+// Back substitution along n frames f = f0, f0 + step, ..:  delta_f = z_f - G_f delta_prev
+// (lane i < 12: row i).  G_f rows and z_f come from the workspace slot of f, loaded one frame
+// ahead (two register sets), except the first frame's G (G0, LDS) when given; delta_prev
+// starts as d0 (LDS) or, without one, the first frame has no coupling term.
+// dl: 12 doubles of LDS scratch (this wave's).
+__device__ __forceinline__ void gn_backsub(const double* ws, int f0, int step, int n, const double* G0,
+                                           const double* d0, double* dl, double* delta, int i) {
+  using namespace gn;
+  if (n <= 0) return;
+  const int ir = i < NV ? i : NV - 1;
+  double Gn[NV], zn;
+  auto ld = [&](int u) __attribute__((always_inline)) {
+    const double* wn = ws + (size_t)(f0 + u * step) * GN_WSF;
+    const double* gr = (u == 0 && G0) ? G0 + ir * NV : wn + ir * NV;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) Gn[k] = gr[k];
+    zn = wn[NB + ir];
+  };
+  if (d0 && i < NV) dl[i] = d0[i];
+  wave_order();
+  ld(0);
+  for (int u = 0; u < n; ++u) {
+    double Gc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) Gc[k] = Gn[k];
+    double d = zn;
+    if (u + 1 < n) ld(u + 1);
+    if (u > 0 || d0) {
+      double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < NV; k += 2) {
+        e0 += Gc[k] * dl[k];
+        e1 += Gc[k + 1] * dl[k + 1];
+      }
+      d -= e0 + e1;
+    }
+    wave_order();
+    if (i < NV) {
+      dl[i] = d;
+      delta[(size_t)(f0 + u * step) * NV + i] = d;
+    }
+    wave_order();
+  }
+}
+
 // SOLVER = 1 (round 3): block Thomas with explicit inverses, so the per-frame chain has ONE
 // 12-step sequence instead of three (W solve, Cholesky, y solve):
 //   G_{l-1} = M_{l-1} E_{l-1}                   (M = S^-1; 12 x 12 x 12, no chain)
@@ -346,12 +583,7 @@ __global__ __launch_bounds__(64 * (NA + 1), 3) void gn_step_kernel(GnArgs a) {
     // the solver's chain is the launch's critical path: it wins issue arbitration against
     // the assembler waves of its own and of the CU's other workgroups
     __builtin_amdgcn_s_setprio(3);
-    __shared__ __attribute__((aligned(16))) double bs[NV];
-    __shared__ __attribute__((aligned(16))) double rk2[2 * NV];  // the sweep's pivot rows k, k + 1
-    double* Mp = Lp;  // M_{l-1}, row-major
-    double* Pb = Wt;  // G_{l-1}
-    double* zp = ys;  // z_{l-1}
-    typedef double d2_t __attribute__((ext_vector_type(2)));
+    __shared__ __attribute__((aligned(16))) GnChainLds C;
     const bool act = i < 36;
     const int ii = act ? i : 35;
     const int r = ii / 3, c0 = 4 * (ii - 3 * (ii / 3));
@@ -361,124 +593,19 @@ __global__ __launch_bounds__(64 * (NA + 1), 3) void gn_step_kernel(GnArgs a) {
       while (lds_load_acquire(&ready[cur]) != l + 1) __builtin_amdgcn_s_sleep(1);
       gn_stamp(a, t, 65 + 4 * l);
       if (!info) {
-        double* wl = ws + (size_t)l * GN_WSF;
         const double* bc = blk[cur];
-        const double* bp = blk[prv];
         double sv[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) sv[c] = bc[r * NV + c0 + c] + (r == c0 + c ? a.lambda : 0.0);
         double b = -bc[2 * NB + r];
-        if (l > 0) {
-          // G_{l-1}[r][c0..] = sum_k M_{l-1}[r][k] E_{l-1}[k][c0..]
-          double pv[4] = {0.0, 0.0, 0.0, 0.0}, ph[4] = {0.0, 0.0, 0.0, 0.0};  // even / odd k
-#pragma unroll
-          for (int k = 0; k < NV; ++k) {
-            const double m = Mp[r * NV + k];
-            const d2_t e0 = *reinterpret_cast<const d2_t*>(bp + NB + k * NV + c0);
-            const d2_t e1 = *reinterpret_cast<const d2_t*>(bp + NB + k * NV + c0 + 2);
-            double* acc = (k & 1) ? ph : pv;
-            acc[0] += m * e0[0];
-            acc[1] += m * e0[1];
-            acc[2] += m * e1[0];
-            acc[3] += m * e1[1];
-          }
-#pragma unroll
-          for (int c = 0; c < 4; ++c) pv[c] += ph[c];
-          wave_order();  // every lane is past its reads of M_{l-1} / G_{l-2}
-          if (act) {
-            *reinterpret_cast<d2_t*>(Pb + r * NV + c0) = d2_t{pv[0], pv[1]};
-            *reinterpret_cast<d2_t*>(Pb + r * NV + c0 + 2) = d2_t{pv[2], pv[3]};
-            double* gw = ws + (size_t)(l - 1) * GN_WSF + r * NV + c0;  // G_{l-1} for the backward pass
-#pragma unroll
-            for (int c = 0; c < 4; ++c) gw[c] = pv[c];
-          }
-          wave_order();
-          // S -= E_{l-1}^T G_{l-1};  b -= E_{l-1}^T z_{l-1}
-          double s2[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}}, b2[2] = {0.0, 0.0};
-#pragma unroll
-          for (int k = 0; k < NV; ++k) {
-            const double ek = bp[NB + k * NV + r];
-            const d2_t p0 = *reinterpret_cast<const d2_t*>(Pb + k * NV + c0);
-            const d2_t p1 = *reinterpret_cast<const d2_t*>(Pb + k * NV + c0 + 2);
-            s2[k & 1][0] += ek * p0[0];
-            s2[k & 1][1] += ek * p0[1];
-            s2[k & 1][2] += ek * p1[0];
-            s2[k & 1][3] += ek * p1[1];
-            b2[k & 1] += ek * zp[k];
-          }
-#pragma unroll
-          for (int c = 0; c < 4; ++c) sv[c] -= s2[0][c] + s2[1][c];
-          b -= b2[0] + b2[1];
-        }
+        if (l > 0)  // G_{l-1} = M_{l-1} E_{l-1} (to the workspace for the backward pass)
+          gn_couple<false>(C.M, C.z, blk[prv] + NB, C.G, ws + (size_t)(l - 1) * GN_WSF, r, c0, act, sv, b);
         gn_stamp(a, t, 66 + 4 * l);
-        // M_l = S_l^-1: symmetric sweep with 2 x 2 pivot blocks K = {k, k + 1}, k = 0, 2, .., 10
-        // (ends with -S^-1):  S_KK <- -P^-1,  S_iK <- S_iK P^-1,  S_Kj <- P^-1 S_Kj,
-        // S_ij <- S_ij - S_iK P^-1 S_Kj  (P = S_KK).  P is positive definite iff a > 0 and
-        // det > 0 -- the two scalar pivots a, d - b^2 / a of the Cholesky / LDL^T test.
-        bool bad = false;
-#pragma unroll 1
-        for (int k = 0; k < NV; k += 2) {
-          if (act && (r >> 1) == (k >> 1)) {  // rows k, k + 1 -> the pivot-row buffer
-            double* dst = rk2 + (r - k) * NV + c0;
-            *reinterpret_cast<d2_t*>(dst) = d2_t{sv[0], sv[1]};
-            *reinterpret_cast<d2_t*>(dst + 2) = d2_t{sv[2], sv[3]};
-          }
-          wave_order();
-          const d2_t pa = *reinterpret_cast<const d2_t*>(rk2 + k);       // S[k][k], S[k][k+1]
-          const double pd = rk2[NV + k + 1];                             // S[k+1][k+1]
-          const double u0 = rk2[r], u1 = rk2[NV + r];                    // S[r][k], S[r][k+1] (symmetric)
-          const d2_t x0 = *reinterpret_cast<const d2_t*>(rk2 + c0);
-          const d2_t x1 = *reinterpret_cast<const d2_t*>(rk2 + c0 + 2);
-          const d2_t y0 = *reinterpret_cast<const d2_t*>(rk2 + NV + c0);
-          const d2_t y1 = *reinterpret_cast<const d2_t*>(rk2 + NV + c0 + 2);
-          const double vk[4] = {x0[0], x0[1], x1[0], x1[1]};   // S[k][c0 ..]
-          const double vk1[4] = {y0[0], y0[1], y1[0], y1[1]};  // S[k+1][c0 ..]
-          double a0 = pa[0], b0 = pa[1], d0 = pd;
-          double det = a0 * d0 - b0 * b0;
-          if (!(a0 > 0.0) || !(det > 0.0)) {
-            bad = true;
-            a0 = 1.0;
-            b0 = 0.0;
-            d0 = 1.0;
-            det = 1.0;
-          }
-          const double id = gn_rcp(det);
-          const double q00 = d0 * id, q01 = -b0 * id, q11 = a0 * id;  // P^-1 (symmetric)
-          // one formula for every element (branch-free): with (al0, al1) = row r - k of P^-1
-          // for the pivot rows and -(S_rK P^-1) otherwise,
-          //   j not in K:  S'[r][j] = (r in K ? 0 : S[r][j]) + al0 S[k][j] + al1 S[k+1][j]
-          //   j in K:      S'[r][j] = -(j == k ? al0 : al1)
-          const bool rk = (r >> 1) == (k >> 1);
-          const double al0 = rk ? (r == k ? q00 : q01) : -(u0 * q00 + u1 * q01);
-          const double al1 = rk ? (r == k ? q01 : q11) : -(u0 * q01 + u1 * q11);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int j = c0 + c;
-            const double gen = fma(al0, vk[c], fma(al1, vk1[c], rk ? 0.0 : sv[c]));
-            sv[c] = (j >> 1) == (k >> 1) ? -(j == k ? al0 : al1) : gen;
-          }
-        }
-        if (bad) {
+        if (!gn_sweep(sv, C.rk2, r, c0, act)) {
           info = l + 1;  // the solver wave idles through the remaining frames' hand-overs
         } else {
-          wave_order();
-          if (act) {
-            *reinterpret_cast<d2_t*>(Mp + r * NV + c0) = d2_t{-sv[0], -sv[1]};
-            *reinterpret_cast<d2_t*>(Mp + r * NV + c0 + 2) = d2_t{-sv[2], -sv[3]};
-            if (c0 == 0) bs[r] = b;
-          }
-          wave_order();
-          double z0 = 0.0, z1 = 0.0;
-#pragma unroll
-          for (int j = 0; j < NV; j += 2) {
-            z0 += Mp[r * NV + j] * bs[j];
-            z1 += Mp[r * NV + j + 1] * bs[j + 1];
-          }
-          wave_order();
-          if (act && c0 == 0) {
-            zp[r] = z0 + z1;
-            wl[NB + r] = z0 + z1;
-          }
+          const double z = gn_finish(sv, b, C, r, c0, act);
+          if (act && c0 == 0) ws[(size_t)l * GN_WSF + NB + r] = z;
         }
       }
       if (i == 0) lds_store_release(&consumed, l + 1);
@@ -486,46 +613,8 @@ __global__ __launch_bounds__(64 * (NA + 1), 3) void gn_step_kernel(GnArgs a) {
     }
     gn_stamp(a, t, 250);
     if (!info) {
-      // backward: delta_l = z_l - G_l delta_{l+1}; lane i < 12: row i.  G rows and z are
-      // read from the workspace two frames ahead (a ring of three register sets), so the
-      // chain waits on the LDS broadcast of delta only, not on memory
-      const int ir = i < NV ? i : NV - 1;
-      double* dl = bs;  // delta_{l+1}
-      double Gq[3][NV], zq[3];
-      auto ld = [&](int l, int slot) __attribute__((always_inline)) {
-        const double* wn = ws + (size_t)l * GN_WSF;
-#pragma unroll
-        for (int k = 0; k < NV; ++k) Gq[slot][k] = wn[ir * NV + k];
-        zq[slot] = wn[NB + ir];
-      };
-      ld(L - 1, (L - 1) % 3);
-      if (L >= 2) ld(L - 2, (L - 2) % 3);
-      for (int l = L - 1; l >= 0; --l) {
-        if (l >= 2) ld(l - 2, (l - 2) % 3);
-        double d = 0.0;
-        // the ring slot is l % 3: a runtime index, so select it with three compile-time branches
-#define GN_BWD(S)                                              \
-  {                                                            \
-    d = zq[S];                                                 \
-    if (l + 1 < L) {                                           \
-      double d0 = 0.0, d1 = 0.0;                               \
-      _Pragma("unroll") for (int k = 0; k < NV; k += 2) {      \
-        d0 += Gq[S][k] * dl[k];                                \
-        d1 += Gq[S][k + 1] * dl[k + 1];                        \
-      }                                                        \
-      d -= d0 + d1;                                            \
-    }                                                          \
-  }
-        const int sl = l % 3;
-        if (sl == 0) GN_BWD(0) else if (sl == 1) GN_BWD(1) else GN_BWD(2)
-#undef GN_BWD
-        wave_order();
-        if (i < NV) {
-          dl[i] = d;
-          a.delta[((size_t)t * L + l) * NV + i] = d;
-        }
-        wave_order();
-      }
+      // backward: delta_l = z_l - G_l delta_{l+1}, l = L - 1 .. 0
+      gn_backsub(ws, L - 1, -1, L, nullptr, nullptr, C.bs, a.delta + (size_t)t * L * NV, i);
     } else {
       for (int e = i; e < L * NV; e += 64) a.delta[(size_t)t * L * NV + e] = NAN;
     }
@@ -692,6 +781,145 @@ __global__ __launch_bounds__(64 * (NA + 1), 3) void gn_step_kernel(GnArgs a) {
   if (a.info && i == 0) a.info[t] = info;
 }
 
+// SOLVER 2 (round 3, shipped): SOLVER 1's block Thomas elimination run from BOTH ends of the
+// trajectory at once (twisted / "burn at both ends" factorization).  Frames 0 .. m - 1 are
+// eliminated top-down by one solver wave and frames L - 1 .. m + 1 bottom-up by another, each
+// fed by its own assembler wave and LDS ring (R = 3 slots, the SOLVER 1 protocol); the top
+// solver then eliminates frame m against both neighbours,
+//   Z_m = D_m + lambda I - E_{m-1}^T M_{m-1} E_{m-1} - E_m N_{m+1} E_m^T,
+//   z_m = Z_m^-1 (-g_m - E_{m-1}^T z_{m-1} - E_m w_{m+1}) = delta_m,
+// and the two back substitutions run outward from delta_m concurrently:
+//   delta_l = z_l - G_l delta_{l+1} (l < m),   delta_l = w_l - H_l delta_{l-1} (l > m),
+// H_l = N_l E_{l-1}^T.  The bottom chain is the top chain's algorithm on the mirrored problem
+// (frame j = L - 1 - l, coupling block E'_{j-1} = E_l^T, read transposed from frame l's own
+// slot: gn_couple<true>); the merge's extra term is one more gn_couple<true> with the bottom
+// chain's N_{m+1}, w_{m+1} and frame m's E_m.  m = L / 2: the serial depth is L - m + 1 frame
+// eliminations (13 at L = 24) instead of L.  Workspace slot l holds G_l, z_l (l <= m) or H_l,
+// w_l (l > m).  Waves: 0 / 1 top / bottom assembler, 2 / 3 top / bottom solver.  info: the
+// bottom chain's failed frame if it failed, else the top chain's (1-based; 0 = solved).
+template <int RP>
+__global__ __launch_bounds__(256, 4) void gn_twisted_kernel(GnArgs a) {
+  using namespace gn;
+  constexpr int BLK = 2 * NB + NV;
+  constexpr int R = 3;
+  __shared__ __attribute__((aligned(16))) GnStage<RP> st[2];
+  __shared__ __attribute__((aligned(16))) double blk[2][R][BLK];  // [chain][slot]
+  __shared__ __attribute__((aligned(16))) GnChainLds ch[2];
+  __shared__ __attribute__((aligned(16))) double Hm[NB];  // H_{m+1} = N_{m+1} E_m^T (the merge)
+  __shared__ int ready[2][R];
+  __shared__ int consumed[2];
+  __shared__ int bdone, binfo, mdone;
+  const int t = blockIdx.x;
+  const int wv = threadIdx.x >> 6;
+  const int i = threadIdx.x & 63;
+  const int L = a.L;
+  const int m = L / 2, nb = L - 1 - m;  // merge frame; bottom-chain frames L - 1 .. m + 1
+  const long f0 = (long)t * L;
+  if (threadIdx.x < 2 * R) (&ready[0][0])[threadIdx.x] = 0;
+  if (threadIdx.x < 2) consumed[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    bdone = 0;
+    binfo = 0;
+    mdone = 0;
+  }
+  __syncthreads();
+  if (wv < 2) {  // assembler of chain wv: top frames 0 .. m, bottom frames L - 1 .. m + 1
+    // the next frame's loads are issued before the current frame is built, so the
+    // factors' memory latency is off the chain
+    const int n = wv == 0 ? m + 1 : nb;
+    GnFrameLoads<RP> nx;
+    if (n > 0) gn_load_frame<RP>(a, f0 + (wv == 0 ? 0 : L - 1), nx);
+    for (int j = 0; j < n; ++j) {
+      const int l = wv == 0 ? j : L - 1 - j;
+      const GnFrameLoads<RP> cu = nx;
+      if (j + 1 < n) gn_load_frame<RP>(a, f0 + (wv == 0 ? l + 1 : l - 1), nx);
+      while (lds_load_acquire(&consumed[wv]) < j - R + 2) __builtin_amdgcn_s_sleep(2);
+      gn_stamp(a, t, 2 * l);
+      gn_build_frame<RP>(a, f0 + l, cu, st[wv], blk[wv][j % R]);
+      if (i == 0) lds_store_release(&ready[wv][j % R], j + 1);
+      gn_stamp(a, t, 2 * l + 1);
+    }
+    return;
+  }
+  const int sc = wv - 2;  // solver chain: 0 top, 1 bottom
+  if (sc == 1 && nb == 0) return;
+  __builtin_amdgcn_s_setprio(3);  // the solvers' chains are the launch's critical path
+  double* ws = a.ws + (size_t)t * L * GN_WSF;
+  double* delta = a.delta + (size_t)t * L * NV;
+  GnChainLds& C = ch[sc];
+  const bool act = i < 36;
+  const int ii = act ? i : 35;
+  const int r = ii / 3, c0 = 4 * (ii - 3 * (ii / 3));
+  int info = 0;
+  const int n = sc == 0 ? m + 1 : nb;
+  for (int j = 0; j < n; ++j) {
+    const int l = sc == 0 ? j : L - 1 - j;
+    const int cur = j % R, prv = (j + R - 1) % R;
+    gn_stamp(a, t, 64 + 4 * l);
+    while (lds_load_acquire(&ready[sc][cur]) != j + 1) __builtin_amdgcn_s_sleep(1);
+    gn_stamp(a, t, 65 + 4 * l);
+    const double* bc = blk[sc][cur];
+    const bool merge = sc == 0 && j == m && nb > 0;
+    bool bfail = false;
+    if (merge) {  // the bottom chain's N_{m+1}, w_{m+1} (or its failure)
+      int bd;
+      while ((bd = lds_load_acquire(&bdone)) == 0) __builtin_amdgcn_s_sleep(1);
+      bfail = bd == 2;
+    }
+    if (!info && !bfail) {
+      double sv[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sv[c] = bc[r * NV + c0 + c] + (r == c0 + c ? a.lambda : 0.0);
+      double b = -bc[2 * NB + r];
+      if (j > 0) {
+        if (sc == 0)  // G_{l-1} = M_{l-1} E_{l-1} -> workspace slot l - 1
+          gn_couple<false>(C.M, C.z, blk[0][prv] + NB, C.G, ws + (size_t)(l - 1) * GN_WSF, r, c0, act, sv, b);
+        else  // H_{l+1} = N_{l+1} E_l^T -> workspace slot l + 1
+          gn_couple<true>(C.M, C.z, bc + NB, C.G, ws + (size_t)(l + 1) * GN_WSF, r, c0, act, sv, b);
+      }
+      if (merge) gn_couple<true>(ch[1].M, ch[1].z, bc + NB, Hm, nullptr, r, c0, act, sv, b);
+      gn_stamp(a, t, 66 + 4 * l);
+      if (!gn_sweep(sv, C.rk2, r, c0, act)) {
+        info = l + 1;  // idles through the remaining frames' hand-overs
+      } else {
+        const double z = gn_finish(sv, b, C, r, c0, act);
+        if (act && c0 == 0) ws[(size_t)l * GN_WSF + NB + r] = z;
+      }
+    }
+    if (i == 0) lds_store_release(&consumed[sc], j + 1);
+    gn_stamp(a, t, 67 + 4 * l);
+  }
+  if (sc == 1) {
+    if (i == 0) {
+      binfo = info;
+      lds_store_release(&bdone, info ? 2 : 1);
+    }
+    int md;
+    while ((md = lds_load_acquire(&mdone)) == 0) __builtin_amdgcn_s_sleep(1);
+    gn_stamp(a, t, 252);
+    if (md == 1)  // delta_l = w_l - H_l delta_{l-1}, l = m + 1 .. L - 1, from delta_m = z_m (top's C.z)
+      gn_backsub(ws, m + 1, 1, nb, Hm, ch[0].z, C.bs, delta, i);
+    else
+      for (int e = i; e < nb * NV; e += 64) delta[(size_t)(m + 1) * NV + e] = NAN;
+    gn_stamp(a, t, 253);
+    return;
+  }
+  // top solver: final info (the bottom chain's failure first), release the bottom solver
+  if (nb > 0) {
+    int bd;
+    while ((bd = lds_load_acquire(&bdone)) == 0) __builtin_amdgcn_s_sleep(1);
+    if (bd == 2) info = lds_load_acquire(&binfo);
+  }
+  if (i == 0) lds_store_release(&mdone, info ? 2 : 1);
+  gn_stamp(a, t, 250);
+  if (!info)  // delta_l = z_l - G_l delta_{l+1}, l = m .. 0 (delta_m = z_m)
+    gn_backsub(ws, m, -1, m + 1, nullptr, nullptr, C.bs, delta, i);
+  else
+    for (int e = i; e < (m + 1) * NV; e += 64) delta[e] = NAN;
+  if (a.info && i == 0) a.info[t] = info;
+  gn_stamp(a, t, 251);
+}
+
 // assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * legacy;
 // 0 = the shipped choice)
 static int g_gn_na = 0;
@@ -707,14 +935,16 @@ static void launch_gn_sv(const GnArgs& a, int na, hipStream_t s) {
   }
 }
 
-// shipped: solver 1 (swept inverses, round 3: 1000 x 24 152 -> 90 us, 3 x 24 123 -> 70 us
-// with the MFMA assembly and batched loads); v & 8 selects the round-2 block Cholesky
+// shipped: solver 2 (the two-ended elimination); v & 16 selects solver 1 (one top-down chain of
+// swept inverses) and v & 8 the round-2 block Cholesky, both with v & 7 assembler waves
 template <int RP>
 static void launch_gn(const GnArgs& a, int v, hipStream_t s) {
   if (v & 8)
     launch_gn_sv<RP, 0>(a, v & 7, s);
-  else
+  else if (v & 16)
     launch_gn_sv<RP, 1>(a, v & 7, s);
+  else
+    hipLaunchKernelGGL((gn_twisted_kernel<RP>), dim3(a.T), dim3(256), 0, s, a);
 }
 
 }  // namespace pa
@@ -727,7 +957,8 @@ int pa_debug_gn_set_trace(unsigned long long* trace_dev) {
 }
 
 int pa_debug_gn_set_assemblers(int na) {
-  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 16, "gn variant %d: assembler waves (0..4) + 8 * legacy solver", na);
+  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 32 && !((na & 8) && (na & 16)),
+           "gn variant %d: assembler waves (0..4) + 8 * legacy Cholesky or 16 * single-chain solver", na);
   pa::g_gn_na = na;
   return PA_OK;
 }

@@ -256,6 +256,27 @@ def test_fp16x3_stride2_variants_agree_bit_for_bit():
     assert torch.equal(y0, y1)
 
 
+def test_fp16x3_merged_steps_match_three_block_form(gold):
+    """fp16x3 3x3 s1 convs: the merged x_hi steps (shipped: x_hi w_hi and x_hi w_lo from one
+    fragment read) against three virtual blocks per 64 channels (variant 70).  The f32
+    accumulation order differs (products interleaved per tap), so agreement is to f32
+    rounding, far below the 1e-3 px bar; both meet the bar against the golden outputs."""
+    name, seed, xn = cases()[0]
+    m = model(seed, precision="fp16x3")
+    x = torch.from_numpy(xn).cuda()
+    xb = torch.from_numpy(synth.synthetic_frames(4, 64)).cuda()
+    y0, yb0 = m(x), m(xb)
+    try:
+        m.set_variants({1: 70, 2: 70, 3: 70, 4: 70})
+        y1, yb1 = m(x), m(xb)
+    finally:
+        m.set_variants({})
+    assert (y0 - y1).abs().max().item() * PX <= 1e-4
+    assert (yb0 - yb1).abs().max().item() * PX <= 1e-4
+    for y in (y0, y1):
+        assert np.abs(y.cpu().numpy() - gold[f"{name}/y_ref_f32"]).max() * PX <= FP32_PX_MAX
+
+
 @pytest.mark.parametrize("B", [1, 3, 64])
 def test_kernel_variants_agree_bit_for_bit(B):
     """The persistent kernels (layer1 weight-resident conv, stride-2 + downsample)
