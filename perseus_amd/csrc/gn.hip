@@ -8,14 +8,16 @@
 //   D_l (diagonal): the K projection factors of frame l (pose), the dynamics factors
 //                   (l-1, l) and (l, l+1), the constant-velocity factors around l;
 //   E_l (x_l rows, x_{l+1} cols): the dynamics and constant-velocity factors (l, l+1).
-// One launch (gn_step_kernel), one three-wave workgroup per trajectory: two assembler
-// waves (frames l = a mod 2) build D_l, E_l, g_l = J^T r from the factors touching frame
-// l (each block has one writer, no atomics) into an LDS ring while the solver wave
-// eliminates frame by frame -- SOLVER 0: block Cholesky (L_l L_l^T = D_l + lambda I -
-// W_l^T W_l, W_l = L_{l-1}^{-1} E_{l-1}) with forward and back substitution; SOLVER 1:
-// block Thomas with the Schur complements inverted by the symmetric sweep operator (one
-// 12-step chain per frame instead of three).  D / E / g are also written out (the API's
-// outputs).  f64 throughout.
+// One launch, one workgroup per trajectory.  Assembler waves build D_l, E_l, g_l = J^T r
+// from the factors touching frame l (each block has one writer, no atomics) into LDS rings
+// while solver waves eliminate frame by frame.  Shipped (gn_twisted_kernel, SOLVER 2): four
+// waves -- a top-down and a bottom-up chain, each one assembler + one solver wave, meeting
+// at frame L / 2 (block Thomas with the Schur complements inverted by the symmetric sweep
+// operator, run from both ends).  Kept as variants (gn_step_kernel): SOLVER 1, the same
+// elimination as one top-down chain fed by NA assembler waves; SOLVER 0, the round-2 block
+// Cholesky (L_l L_l^T = D_l + lambda I - W_l^T W_l, W_l = L_{l-1}^{-1} E_{l-1}) with
+// forward and back substitution.  D / E / g are also written out (the API's outputs).
+// f64 throughout.
 // Jacobians are column-major per factor (include/perseus_amd.h).
 #include "common.h"
 
