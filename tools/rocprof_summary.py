@@ -25,7 +25,7 @@ import json
 import os
 import shutil
 import statistics
-from collections import defaultdict
+from collections import defaultdict, Counter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -140,18 +140,25 @@ def main():
                 line_ = (f"Agreement: bench roofline kernel `{roof['kernel']}` avg {roof['avg_ms'] * 1e3:.2f} us per "
                          f"launch (HIP events, back-to-back reps)")
                 btr = find(os.path.join(a.dir, "bench_kt"), "*kernel_trace.csv")
-                if btr and syms:
-                    # the bench command also runs these kernels at B = 1024 (its configs[2] leg), so
-                    # --stats' per-symbol average mixes batch sizes; the median over the same
-                    # command's dispatches is the B = 64 launch (the majority of dispatches)
+                ftr = find(os.path.join(a.dir, "fwd_kt"), "*kernel_trace.csv")
+                if btr and ftr and syms:
+                    # the bench command also runs these kernels at other batches (configs[2]'s
+                    # 1,024-frame chunks, the streaming leg's 3-frame ticks), so --stats' per-symbol
+                    # average mixes batch sizes: keep the dispatches whose grid is the one the
+                    # plain B-frame forwards launch
+                    grid = defaultdict(Counter)
+                    for r in csv.DictReader(open(ftr)):
+                        grid[r["Kernel_Name"]][r["Grid_Size_X"]] += 1
                     per = defaultdict(list)
                     for r in csv.DictReader(open(btr)):
-                        per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                        g = grid.get(r["Kernel_Name"])
+                        if g and r["Grid_Size_X"] == g.most_common(1)[0][0]:
+                            per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
                     if all(syms[i] in per for i in idx):
                         st = sum(statistics.median(per[syms[i]]) for i in idx) / len(idx)
                         n = sum(len(per[syms[i]]) for i in idx)
                         line_ += (f"; rocprofv3 --kernel-trace of the same bench command, median over its {n} "
-                                  f"dispatches of the kernel: {st:.2f} us")
+                                  f"dispatches of the kernel at the B = {B} grid: {st:.2f} us")
                 line_ += f"; kernel trace of plain forwards (cold-er caches): {rp:.2f} us."
                 lines.append(line_)
     # fp16x3 parity-mode forwards (tools/pmc_forward.py --precision fp16x3 --out DIR/x3)
