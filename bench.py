@@ -143,6 +143,7 @@ def main():
     line = None
     if rank == 0:
         roof = roofline(per_launch, B, args.precision)
+        per_kernel = per_kernel_rooflines(per_launch, B, args.precision)
         # rank 0 at every world size, after the timed region (the other ranks wait at the
         # closing barrier): the driver's N = 1..8 lines each carry the CPU baseline
         cpu = None if args.no_cpu_baseline else cpu_baseline(state, x_host)
@@ -174,6 +175,7 @@ def main():
             "streaming": stream,
             "cpu_baseline": cpu,
             "kernels_ms": {f"{i:02d}_{n}": round(ms, 4) for i, n, ms in per_launch},
+            "per_kernel_roofline": per_kernel,
             "factors": fac,
         }
         print(json.dumps(line))
@@ -391,6 +393,31 @@ def roofline(per_launch, B, precision):
     return {"kernel": name, "bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": peak / 1e12,
             "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic, "launches": n,
             "avg_ms": round(ms / n, 5), "flops_per_launch": f / n}
+
+
+def per_kernel_rooflines(per_launch, B, precision):
+    """north_star's per-kernel figures: the conv stem's achieved HBM GB/s (algorithmic
+    bytes: the f32 NCHW input it reads, the pooled fp16 NHWC map it writes, its packed
+    fp16 weights) against the 8 TB/s peak, with the PMC bytes of that launch when the
+    committed record matches these kernels; and every 3x3 conv launch's MFMA utilisation
+    (algorithmic FLOPs / launch time) against the dense fp16 peak."""
+    if precision != "fp16" or not per_launch or per_launch[0][1] != "stem_conv7x7_pool":
+        return None
+    fl = conv_flops(B, fused_stem=True, fused_ds=True, fused_head=per_launch[-1][1] != "avgpool_fc")
+    if len(fl) != len(per_launch):
+        return None
+    names = [nm for _, nm, _ in per_launch]
+    stem_ms = per_launch[0][2]
+    stem_bytes = B * 4 * 256 * 256 * 4 + B * 64 * 64 * 64 * 2 + 64 * 7 * 32 * 2
+    stem = {"kernel": per_launch[0][1], "bound": "hbm", "us": round(stem_ms * 1e3, 2), "alg_bytes": stem_bytes,
+            "achieved_gbps": round(stem_bytes / (stem_ms * 1e-3) / 1e9, 1),
+            "frac": round(stem_bytes / (stem_ms * 1e-3) / HBM_PEAK, 4), "peak_gbps": HBM_PEAK / 1e9,
+            "pmc_bytes": pmc_traffic(precision, B, [per_launch[0][0]], names),
+            "mfma_frac": round(fl[0] / (stem_ms * 1e-3) / MFMA_FP16_DENSE_PEAK, 4)}
+    convs = {f"{i:02d}_{nm}": round(f / (ms * 1e-3) / MFMA_FP16_DENSE_PEAK, 4)
+             for (i, nm, ms), f in zip(per_launch, fl) if nm.startswith("conv3x3")}
+    return {"stem": stem, "conv3x3_mfma_frac": convs, "mfma_peak_tflops": MFMA_FP16_DENSE_PEAK / 1e12,
+            "timing": "per-launch HIP events (pa_detector_time_launch), as kernels_ms"}
 
 
 def factor_leg(dev, seed, rank, T=1000, L=24, reps=20):
