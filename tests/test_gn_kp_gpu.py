@@ -48,3 +48,38 @@ def test_gn_step_other_keypoint_counts(corners):
 def test_gn_step_many_trajectories():
     """600 trajectories: several workgroups per CU, slot reuse over 13 frames."""
     _check(CORNERS, 600, 13, 1e-2, 4)
+
+
+@pytest.mark.parametrize("L", [2, 3, 4, 25])
+def test_gn_step_short_and_odd_windows(L):
+    """The two-ended elimination's edge cases (gn_twisted_kernel, merge frame m = L / 2): L = 2
+    has no bottom chain, L = 3 a one-frame bottom chain, L = 25 chains of unequal length."""
+    _check(CORNERS, 5, L, 1e-3, 30 + L)
+
+
+def test_gn_step_more_trajectories_than_one_round():
+    """1,100 trajectories: more four-wave workgroups than one round holds at four per CU."""
+    _check(CORNERS, 1100, 6, 1e-2, 8)
+
+
+@pytest.mark.parametrize("variant", [16 + 2, 8 + 2])
+def test_gn_step_solver_variants_agree(variant):
+    """The single-chain solver (16 + NA) and the round-2 block Cholesky (8 + NA), kept as
+    pa_debug_gn_set_assemblers variants, against the shipped two-ended kernel."""
+    from perseus_amd import _lib
+
+    poses, vels, angvels, _ = _problem(4, 24, 3)
+    y = np.random.default_rng(4).uniform(-1, 1, (4 * 24, 16)).astype(np.float32)
+    lin = pipeline.linearize_trajectories(torch.as_tensor(y, device="cuda"), poses, vels, angvels, CORNERS, KCAL,
+                                          T=4, L=24, dt=0.1, proj_sigmas=np.array([2.0, 2.0]),
+                                          dyn_sigmas=np.full(6, 0.05), cv_sigmas=np.full(3, 0.5))
+    ref = pipeline.gn_step(lin, T=4, L=24, lam=1e-3)
+    L_ = _lib.lib()
+    try:
+        _lib.check(L_.pa_debug_gn_set_assemblers(variant))
+        out = pipeline.gn_step(lin, T=4, L=24, lam=1e-3)
+    finally:
+        _lib.check(L_.pa_debug_gn_set_assemblers(0))
+    d0, d1 = ref["delta"].cpu().numpy(), out["delta"].cpu().numpy()
+    np.testing.assert_allclose(d1, d0, rtol=1e-7, atol=1e-9 * np.abs(d0).max())
+    assert torch.equal(ref["D"], out["D"]) and torch.equal(ref["g"], out["g"])
