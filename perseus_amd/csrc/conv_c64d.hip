@@ -222,11 +222,24 @@ static int num_cus_d() {
   return n;
 }
 
+// CUs the launch stream may use: a stream created with a CU mask (hipExtStreamCreateWithCUMask,
+// e.g. two half-batches on disjoint halves of every XCD) gets one persistent workgroup per CU
+// of its mask, not of the device
+static int stream_cus(hipStream_t s) {
+  const int all = num_cus_d();
+  uint32_t m[32] = {};
+  if (hipExtStreamGetCUMask(s, 32, m) != hipSuccess) return all;
+  int n = 0;
+  for (int i = 0; i < 32; ++i) n += __builtin_popcount(m[i]);
+  return (n > 0 && n < all) ? n : all;
+}
+
 template <int DBG, bool WT = false>
 static int run_c64d(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * 64 * 2 < 0x7fffffffu, "c64d conv: output over 2 GB");
   const int tiles = a.B * (a.Hout / c64d::TH) * (a.Wout / c64d::TW);
-  const int grid = tiles < num_cus_d() ? tiles : num_cus_d();
+  const int cus = stream_cus(s);
+  const int grid = tiles < cus ? tiles : cus;
   if (a.epi & EPI_RES)
     hipLaunchKernelGGL((conv3x3_c64d<EPI_RELU | EPI_RES, DBG, WT>), dim3(grid), dim3(512), 0, s, a, tiles);
   else
