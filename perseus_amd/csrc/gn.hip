@@ -356,14 +356,14 @@ struct GnChainLds {
 // with E'(k, c) = eb[k * NV + c] (MIR = false: E_{l-1}, from the previous frame's slot) or
 // eb[c * NV + k] (MIR = true: the current frame's own E_l, transposed -- the bottom-up chain).
 // G goes to Gout (LDS) and, when gws is given, to the workspace (row-major, back substitution).
-template <bool MIR>
+template <bool MIR, int CU = GN_CU>
 __device__ __forceinline__ void gn_couple(const double* Mprev, const double* zprev, const double* eb, double* Gout,
                                           double* gws, int r, int c0, bool act, double (&sv)[4], double& b) {
   using namespace gn;
   double pv[4] = {0.0, 0.0, 0.0, 0.0}, ph[4] = {0.0, 0.0, 0.0, 0.0};  // even / odd k
   // k in pairs, the pair loop unrolled by NU only: fully unrolled, the compiler hoists all
   // 60 LDS reads and the 4-wave workgroup's 128-VGPR budget spills
-#pragma unroll GN_CU
+#pragma unroll CU
   for (int k2 = 0; k2 < NV; k2 += 2) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -398,7 +398,7 @@ __device__ __forceinline__ void gn_couple(const double* Mprev, const double* zpr
   }
   wave_order();
   double s2[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}}, b2[2] = {0.0, 0.0};
-#pragma unroll GN_CU
+#pragma unroll CU
   for (int k2 = 0; k2 < NV; k2 += 2) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -799,8 +799,11 @@ __global__ __launch_bounds__(64 * (NA + 1), 3) void gn_step_kernel(GnArgs a) {
 // eliminations (13 at L = 24) instead of L.  Workspace slot l holds G_l, z_l (l <= m) or H_l,
 // w_l (l > m).  Waves: 0 / 1 top / bottom assembler, 2 / 3 top / bottom solver.  info: the
 // bottom chain's failed frame if it failed, else the top chain's (1-based; 0 = solved).
-template <int RP>
-__global__ __launch_bounds__(256, 4) void gn_twisted_kernel(GnArgs a) {
+// OCC workgroups per CU: 4 (k loops unrolled by pairs, <= 128 VGPRs) for launches of more
+// trajectories than 2 per CU, else 2 (fully unrolled, <= 256 VGPRs: a shorter solver chain)
+template <int RP, int OCC = 4>
+__global__ __launch_bounds__(256, OCC) void gn_twisted_kernel(GnArgs a) {
+  constexpr int CU = OCC >= 4 ? GN_CU : 6;
   using namespace gn;
   constexpr int BLK = 2 * NB + NV;
   constexpr int R = 3;
@@ -875,11 +878,11 @@ __global__ __launch_bounds__(256, 4) void gn_twisted_kernel(GnArgs a) {
       double b = -bc[2 * NB + r];
       if (j > 0) {
         if (sc == 0)  // G_{l-1} = M_{l-1} E_{l-1} -> workspace slot l - 1
-          gn_couple<false>(C.M, C.z, blk[0][prv] + NB, C.G, ws + (size_t)(l - 1) * GN_WSF, r, c0, act, sv, b);
+          gn_couple<false, CU>(C.M, C.z, blk[0][prv] + NB, C.G, ws + (size_t)(l - 1) * GN_WSF, r, c0, act, sv, b);
         else  // H_{l+1} = N_{l+1} E_l^T -> workspace slot l + 1
-          gn_couple<true>(C.M, C.z, bc + NB, C.G, ws + (size_t)(l + 1) * GN_WSF, r, c0, act, sv, b);
+          gn_couple<true, CU>(C.M, C.z, bc + NB, C.G, ws + (size_t)(l + 1) * GN_WSF, r, c0, act, sv, b);
       }
-      if (merge) gn_couple<true>(ch[1].M, ch[1].z, bc + NB, Hm, nullptr, r, c0, act, sv, b);
+      if (merge) gn_couple<true, CU>(ch[1].M, ch[1].z, bc + NB, Hm, nullptr, r, c0, act, sv, b);
       gn_stamp(a, t, 66 + 4 * l);
       if (!gn_sweep(sv, C.rk2, r, c0, act)) {
         info = l + 1;  // idles through the remaining frames' hand-overs
@@ -925,6 +928,16 @@ __global__ __launch_bounds__(256, 4) void gn_twisted_kernel(GnArgs a) {
 // assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * legacy;
 // 0 = the shipped choice)
 static int g_gn_na = 0;
+static int g_gn_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
 static unsigned long long* g_gn_trace = nullptr;
 
 template <int RP, int SV>
@@ -945,8 +958,10 @@ static void launch_gn(const GnArgs& a, int v, hipStream_t s) {
     launch_gn_sv<RP, 0>(a, v & 7, s);
   else if (v & 16)
     launch_gn_sv<RP, 1>(a, v & 7, s);
+  else if (v & 32 || a.T > 2 * g_gn_cus())  // 32: force the 4-per-CU form
+    hipLaunchKernelGGL((gn_twisted_kernel<RP, 4>), dim3(a.T), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((gn_twisted_kernel<RP>), dim3(a.T), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gn_twisted_kernel<RP, 2>), dim3(a.T), dim3(256), 0, s, a);
 }
 
 }  // namespace pa
@@ -959,8 +974,9 @@ int pa_debug_gn_set_trace(unsigned long long* trace_dev) {
 }
 
 int pa_debug_gn_set_assemblers(int na) {
-  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 32 && !((na & 8) && (na & 16)),
-           "gn variant %d: assembler waves (0..4) + 8 * legacy Cholesky or 16 * single-chain solver", na);
+  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 64 && !((na & 8) && (na & 16)),
+           "gn variant %d: assembler waves (0..4) + 8 * legacy Cholesky or 16 * single-chain solver, 32: "
+           "two-ended kernel in its 4-per-CU form", na);
   pa::g_gn_na = na;
   return PA_OK;
 }
