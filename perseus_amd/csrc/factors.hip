@@ -885,27 +885,61 @@ __global__ __launch_bounds__(128, 2) void traj_all_kernel(pa_traj_args a, int mo
 // reference leaves to downstream GTSAM code (scripts/streaming.py:121-155 runs the
 // detector only), restated on device so a tick's poses never leave HBM.
 
-// Advance: one workgroup per trajectory.  Thread e moves element e of every per-frame
-// record one frame towards l = 0 (reads frame l + 1 before writing frame l: no other
-// thread touches element e), then thread 0 predicts the new last frame with the
+// Advance: one workgroup per trajectory.  Every element of frames 1 .. L-1 (y, pose, angvel,
+// vel) moves one frame towards l = 0: the 256 threads first load up to ADV_E elements each
+// (all loads in flight at once), then, after a barrier, store them one frame down; rounds
+// cover the window in increasing frame order, so no round stores into what a later round
+// reads.  (Round 2's per-element loop waited out one load-store round trip per frame: 18.7
+// us for 3 x 24 against ~2.)  Then thread 0 predicts the new last frame with the
 // PoseDynamicsFactor model (factors.py:100-105): pose[L-1] = pose[L-2] Exp(dt [w; v_b]),
 // v_b = R^T v for a world-frame velocity; angvel / vel carried over.
-__global__ __launch_bounds__(64) void window_advance_kernel(int L, int n_kp, const float* __restrict__ y_new,
-                                                            float* y, double* pose, double* angvel, double* vel,
-                                                            double dt, int vel_frame) {
+constexpr int ADV_E = 4;
+__global__ __launch_bounds__(256) void window_advance_kernel(int L, int n_kp, const float* __restrict__ y_new,
+                                                             float* y, double* pose, double* angvel, double* vel,
+                                                             double dt, int vel_frame) {
   const int t = blockIdx.x, e = threadIdx.x;
   const int ny = 2 * n_kp;
   float* yt = y + (size_t)t * L * ny;
   double* pt = pose + (size_t)t * L * 12;
   double* wt = angvel + (size_t)t * L * 3;
   double* vt = vel + (size_t)t * L * 3;
-  for (int l = 0; l + 1 < L; ++l) {
-    if (e < ny) yt[l * ny + e] = yt[(l + 1) * ny + e];
-    if (e < 12) pt[l * 12 + e] = pt[(l + 1) * 12 + e];
-    if (e < 3) {
-      wt[l * 3 + e] = wt[(l + 1) * 3 + e];
-      vt[l * 3 + e] = vt[(l + 1) * 3 + e];
+  const int per = ny + 18;        // elements per frame: y (ny floats) | pose (12) | angvel (3) | vel (3)
+  const int n = (L - 1) * per;    // elements of frames 1 .. L-1, frame-major
+  // element k of source frame l + 1 (k < per): its address
+  auto at = [&](int l, int k, bool& isf) -> void* {
+    isf = k < ny;
+    if (k < ny) return yt + (size_t)l * ny + k;
+    k -= ny;
+    if (k < 12) return pt + (size_t)l * 12 + k;
+    k -= 12;
+    if (k < 3) return wt + (size_t)l * 3 + k;
+    return vt + (size_t)l * 3 + (k - 3);
+  };
+  for (int base = 0; base < n; base += 256 * ADV_E) {
+    double v[ADV_E];
+#pragma unroll
+    for (int u = 0; u < ADV_E; ++u) {
+      const int i = base + u * 256 + e;
+      if (i < n) {
+        bool isf;
+        const void* src = at(i / per + 1, i % per, isf);
+        v[u] = isf ? (double)*(const float*)src : *(const double*)src;
+      }
     }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < ADV_E; ++u) {
+      const int i = base + u * 256 + e;
+      if (i < n) {
+        bool isf;
+        void* dst = at(i / per, i % per, isf);
+        if (isf)
+          *(float*)dst = (float)v[u];  // exact: v came from a float
+        else
+          *(double*)dst = v[u];
+      }
+    }
+    __syncthreads();
   }
   if (e < ny) yt[(L - 1) * ny + e] = y_new[(size_t)t * ny + e];
   __syncthreads();
@@ -966,7 +1000,7 @@ int pa_window_advance(int T, int L, int n_kp, const float* y_new, float* y, doub
   if (T == 0) return PA_OK;
   PA_CHECK(y_new && y && pose && angvel && vel, "null pointer");
   PA_CHECK(vel_frame == PA_VEL_WORLD || vel_frame == PA_VEL_BODY, "vel_frame must be 'world' or 'body'.");
-  hipLaunchKernelGGL(pa::window_advance_kernel, dim3(T), dim3(64), 0, (hipStream_t)stream, L, n_kp, y_new, y, pose,
+  hipLaunchKernelGGL(pa::window_advance_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, L, n_kp, y_new, y, pose,
                      angvel, vel, dt, vel_frame);
   PA_LAUNCH_CHECK();
   return PA_OK;
