@@ -65,6 +65,15 @@ int pa_detector_reserve(pa_detector* d, int max_batch);
 /* PA_PREC_FP16 (default), PA_PREC_FP32 or PA_PREC_FP16X3. */
 int pa_detector_set_precision(pa_detector* d, int precision);
 
+/* Latency mode for small batches (the streaming pose stage, streaming.py:101-166: one
+ * frame per camera per tick).  fp16 forwards of B <= max_batch frames run the convs of
+ * layers 2-4 as split-K launches + a fixed-order reduce (layer2's stride-2 entry, with
+ * 64 input channels, on one-tile workgroups instead), which fills the chip at a few
+ * frames (deterministic, but not bit-identical to the batched kernels: the
+ * f32 sums are taken in another order).  Allocates max_batch MiB of partials.
+ * max_batch = 0 (default) turns it off; at most 64. */
+int pa_detector_set_split_k(pa_detector* d, int max_batch);
+
 /* Replaces KeypointCNN.forward (models.py:34-40): x (B,C,H,W) f32 NCHW contiguous
  * on the device -> y (B, 2K) f32, y[:,2k] = x_k, y[:,2k+1] = y_k in [-1,1]
  * normalized image coordinates.  B = 0 is a no-op. */

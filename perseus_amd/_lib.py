@@ -45,6 +45,7 @@ _SIGS = {
     "pa_detector_destroy": (None, [C.c_void_p]),
     "pa_detector_reserve": (C.c_int, [C.c_void_p, C.c_int]),
     "pa_detector_set_precision": (C.c_int, [C.c_void_p, C.c_int]),
+    "pa_detector_set_split_k": (C.c_int, [C.c_void_p, C.c_int]),
     "pa_detector_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
     "pa_detector_profile": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p, C.c_int]),

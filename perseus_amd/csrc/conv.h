@@ -53,6 +53,9 @@ struct ConvArgs {
   const float* fcw;
   const float* fcb;
   float* y;
+  // split-K mode (conv_gx.h PART, small batches): f32 partial sums [split][B][Hout][Wout][Cout],
+  // split = blockIdx.y over the input-channel blocks
+  float* part;
 };
 
 // conv3x3 s2 (+bn, relu) -> out and 1x1 s2 downsample (+bn) -> out2, one pass
@@ -68,6 +71,8 @@ struct ConvS2Args {
   void* out2;          // NHWC [B][Hout][Wout][Cout]
   int B, Hin, Win, Cin, Hout, Wout, Cout;
   unsigned long long* trace;  // as ConvArgs::trace
+  // split-K mode (conv_s2x.h PART): f32 partials [2][split][B][Hout][Wout][Cout] (conv, then downsample)
+  float* part;
 };
 
 template <typename T>
@@ -88,6 +93,13 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname);
 int launch_conv3x3_gx_l2(const ConvArgs& a, int variant, hipStream_t s);
 int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s);
 int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s);
+// the same convs split-K + a fixed-order reduce (small batches, conv_splitk.hip): a.part
+// holds splitk_part_floats(B) floats
+int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s);
+// stride-2 block entries for small batches: layer2 on one-tile workgroups, layer4 split-K with
+// the conv and the downsample reduced in one pass (layer3's batched kernel is kept)
+int launch_conv3x3s2_small(const ConvS2Args& a, hipStream_t s, const char** kname);
+size_t splitk_part_floats(int B);
 
 // layer1 (Cin = Cout = 64), fp16: weight-resident persistent kernel (conv_c64.hip)
 int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s);

@@ -258,12 +258,21 @@ __device__ __forceinline__ HiLo split_x3(float v) {
   return HiLo{h, (_Float16)(v - (float)h)};
 }
 
+// PART = NS > 0 (split-K for small batches, conv_splitk.hip): the workgroup runs the CIN
+// (= 64 * NCB) input channels of split blockIdx.y of an a.Cin = NS * CIN channel conv and
+// writes its f32 accumulators to a.part[split] -- no bias, residual or ReLU (splitk_reduce
+// applies them after summing the splits in order).  The K loop is 1 / NS of the full
+// conv's, which is the launch's critical path when a batch of a few frames gives every CU at
+// most one workgroup.  (A fix-up in the same launch -- write-through partials, a per-tile
+// arrival counter, the last arriver summing -- measured slower than the separate reduce:
+// 15-19 us against 9 + 4.7 us at B = 3)
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1,
-          bool WT = true, bool X3 = false, bool XM = false>
+          bool WT = true, bool X3 = false, bool XM = false, int PART = 0>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
   static_assert(!XM || (X3 && FD == 1), "merged X3 steps: fp16x3, fragments half a step ahead");
+  static_assert(!PART || (!X3 && EPI == 0), "split-K partials: fp16, no epilogue");
   using VB = GxBlocks<X3, NCB, XM>;
   constexpr int XS = X3 ? 2 : 1;  // fp16 planes per activation / weight element
   constexpr int NSTEPS = VB::NVB * 9;
@@ -288,7 +297,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   // slot (t + PD) % NSLOT, written at step t, was last read by step t + PD - NSLOT,
   // which must lie before the last barrier: t - G with a barrier every G steps
   constexpr int NSLOT = PD + G;
-  constexpr int RL = XS * TN + ((EPI & EPI_RES) ? XS * TM * TN / 2 : 0);
+  constexpr int RL = PART ? 0 : XS * TN + ((EPI & EPI_RES) ? XS * TM * TN / 2 : 0);
   // epilogue loads (bias, residual) issued RSD steps before the end: early enough to
   // land, late enough not to hold their VGPRs across the whole K loop
   constexpr int RSD = 4;
@@ -303,8 +312,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int q = lane >> 4, r16 = lane & 15;
   const int H = a.Hout, W = a.Wout;
-  const _Float16* __restrict__ in = (const _Float16*)a.in;
-  const _Float16* __restrict__ w = (const _Float16*)a.w;
+  // PART: pixel stride and weight tap stride are the full conv's a.Cin; split blockIdx.y
+  // starts at input channel CIN * blockIdx.y
+  const int kin = PART ? a.Cin : KW;
+  const int kc0 = PART ? CIN * (int)blockIdx.y : 0;
+  const _Float16* __restrict__ in = (const _Float16*)a.in + kc0;
+  const _Float16* __restrict__ w = (const _Float16*)a.w + kc0;
 
   const int Cout = a.Cout;
   const int ntn = Cout / BN;
@@ -343,7 +356,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     const int pr = pp / PW, pcl = pp - (pp / PW) * PW;
     const int n = img0 + img, h = th0 + pr - 1, x = tw0 + pcl - 1;
     const bool ok = p < NP && pr < PH && n < a.B && (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W;
-    psrc[i] = ok ? (const char*)(in + (((size_t)n * H + h) * W + x) * KW + lc * 8) : nullptr;
+    psrc[i] = ok ? (const char*)(in + (((size_t)n * H + h) * W + x) * kin + lc * 8) : nullptr;
   }
   auto dma_patch = [&](int vb, int buf) __attribute__((always_inline)) {
 #pragma unroll
@@ -357,17 +370,17 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   for (int i = 0; i < WDMA; ++i) {
     const int c = (i * NW + wid) * 64 + lane;
     const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
-    wsrc[i] = w + (size_t)(n0 + xperm(co)) * KTOT + lc * 8;
+    wsrc[i] = w + (size_t)(n0 + xperm(co)) * (PART ? 9 * kin : KTOT) + lc * 8;
   }
   auto dma_w = [&](int s) __attribute__((always_inline)) {
     const int vb = s / 9, tap = s % 9;
 #pragma unroll
     for (int i = 0; i < WDMA; ++i)
-      xdma16(wsrc[i] + tap * KW + VB::wblk(vb) * 64, wring + (s % NSLOT) * WSLOT + (i * NW + wid) * 1024);
+      xdma16(wsrc[i] + tap * kin + VB::wblk(vb) * 64, wring + (s % NSLOT) * WSLOT + (i * NW + wid) * 1024);
     if (VB::two(vb))  // compile-time after inlining (s is a step constant)
 #pragma unroll
       for (int i = 0; i < WDMA; ++i)
-        xdma16(wsrc[i] + tap * KW + VB::wblk2(vb) * 64, wring + (s % NSLOT) * WSLOT + WB + (i * NW + wid) * 1024);
+        xdma16(wsrc[i] + tap * kin + VB::wblk2(vb) * 64, wring + (s % NSLOT) * WSLOT + WB + (i * NW + wid) * 1024);
   };
 
   const int o = xfrag(r16);
@@ -498,7 +511,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + PD < NSTEPS && (DBG < 2 || DBG == 5)) dma_w(S + PD);
     if constexpr (CB + 1 < VB::NVB && S == plan.ps(CB + 1) && (DBG < 2 || DBG == 5)) dma_patch(CB + 1, (CB + 1) & 1);
-    if constexpr (S == plan.rs) {
+    if constexpr (S == plan.rs && !PART) {
       // vm_after() counts these after this step's DMAs: keep the scheduler from
       // moving the (read-only) loads across them
       __builtin_amdgcn_sched_barrier(0);
@@ -522,6 +535,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
 
   if constexpr (EPI & EPI_HEAD) {
     gx_head<TH, TW, NI, BN, NT, WTM, WTN, TM, TN, EPI>(a, smem, acc, bias, rv, img0, n0, ntn, o);
+    return;
+  }
+  if constexpr (PART > 0) {  // f32 partials: acc[tm][tn] = 4 consecutive output channels of one pixel
+    float* __restrict__ pt = a.part + (size_t)blockIdx.y * a.B * H * W * Cout;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      if (!ok[tm]) continue;
+      const size_t pix = pixo[tm] / Cout;  // (n * H + y) * W + x (XS = 1: pixo = pix * Cout + channel < Cout)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int c = n0 + wn * WTN + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4;
+        *reinterpret_cast<f32x4*>(pt + pix * Cout + c) = acc[tm][tn];
+      }
+    }
     return;
   }
 #pragma unroll
@@ -554,6 +581,19 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     __builtin_amdgcn_s_waitcnt(0);
     trace_stamp(a.trace, 63);
   }
+}
+
+// split-K partial launch (PART = NS): grid.y = NS splits of CIN channels, f32 partials to a.part
+template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int NS>
+static int run_gx_part(const ConvArgs& a, hipStream_t s) {
+  PA_CHECK(a.part && a.Cin == NS * CIN && a.Hout == a.Hin && a.Hout % TH == 0 && a.Wout % TW == 0 && a.Cout % BN == 0,
+           "gx split-K: Cin %d Cout %d %dx%d", a.Cin, a.Cout, a.Hout, a.Wout);
+  const int ntn = a.Cout / BN;
+  const int nsp = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW);
+  hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, 1, 0, 0, 1, true, false, false, NS>), dim3(nsp * ntn, NS),
+                     dim3(WM * WN * 64), 0, s, a, 0);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
 }
 
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1,

@@ -37,8 +37,12 @@ namespace pa {
 // DBG = 4: s_memrealtime stamps into a.trace (conv.h trace_stamp: 0 start, 1 prologue landed,
 // 2 K loop done, 3 epilogue stores issued, 63 stores retired; TPW > 1: 4 + j tile j + 1's
 // first step)
+// PART = NS > 0 (split-K for small batches, conv_splitk.hip): as conv_gx.h's PART, the
+// workgroup runs input channels CIN * blockIdx.y .. of an a.Cin = NS * CIN channel conv and
+// writes its f32 accumulators (conv -> a.part[split], downsample -> a.part[NS + split]),
+// no epilogue
 template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G, bool WT = true, bool X3 = false, int DBG = 0,
-          int TPW = 1>
+          int TPW = 1, int PART = 0>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
@@ -67,7 +71,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile");
   static_assert(G >= 1 && G <= 3 && PD >= G + 1 && PD <= 8, "prefetch distance / steps per barrier");
   constexpr int NSLOT = PD + G;
-  constexpr int RL = TPW > 1 ? 0 : 2 * XS * TN;  // epilogue loads in the stream: bias, bias2 (+ scale, scale2)
+  static_assert(!PART || (TPW == 1 && !X3), "split-K partials: fp16, one tile per workgroup");
+  constexpr int RL = (TPW > 1 || PART) ? 0 : 2 * XS * TN;  // epilogue loads in the stream: bias, bias2 (+ scale, scale2)
   constexpr int RSD = 4;
   constexpr int NST = TM * (TN / 2) * 2 * XS;  // output stores per tile (out, out2; hi, lo)
   constexpr GxPlan plan{NSTEPS, NBLK, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, SPB,
@@ -81,9 +86,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int q = lane >> 4, r16 = lane & 15;
   const int H = a.Hout, W = a.Wout, Hin = a.Hin, Win = a.Win, Cout = a.Cout;
-  const _Float16* __restrict__ in = (const _Float16*)a.in;
-  const _Float16* __restrict__ w = (const _Float16*)a.w;
-  const _Float16* __restrict__ wds = (const _Float16*)a.wds;
+  // PART: pixel and tap strides are the full conv's a.Cin; split blockIdx.y starts at input
+  // channel CIN * blockIdx.y
+  const int kin = PART ? a.Cin : KW;
+  const int kc0 = PART ? CIN * (int)blockIdx.y : 0;
+  const _Float16* __restrict__ in = (const _Float16*)a.in + kc0;
+  const _Float16* __restrict__ w = (const _Float16*)a.w + kc0;
+  const _Float16* __restrict__ wds = (const _Float16*)a.wds + kc0;
 
   const int ntn = Cout / BN;
   int tn_idx, sp;  // sp: the workgroup's group of TPW consecutive spatial tiles
@@ -121,7 +130,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
       const int col = pos <= TW ? 2 * pos : 2 * (pos - TW - 1) + 1;
       const int h = 2 * th0 - 1 + pr, x = 2 * tw0 - 1 + col;
       const bool ok = p < NP && pos < 2 * TW + 1 && (unsigned)h < (unsigned)Hin && (unsigned)x < (unsigned)Win;
-      const char* s = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * KW + lc * 8) + VB::pblk(vb) * 128
+      const char* s = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * kin + lc * 8) + VB::pblk(vb) * 128
                          : (const char*)gx_zero_line;
       xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
     }
@@ -133,15 +142,15 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   for (int i = 0; i < WDMA; ++i) {
     const int c = (i * NW + wid) * 64 + lane;
     const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
-    wsrc[i] = w + (size_t)(n0 + xperm(co)) * KTOT + lc * 8;
-    dsrc[i] = wds + (size_t)(n0 + xperm(co)) * KW + lc * 8;
+    wsrc[i] = w + (size_t)(n0 + xperm(co)) * (PART ? 9 * kin : KTOT) + lc * 8;
+    dsrc[i] = wds + (size_t)(n0 + xperm(co)) * kin + lc * 8;
   }
   auto dma_w = [&](int s) __attribute__((always_inline)) {
     const int vb = (s % SPT) / SPB, t = s % SPB;
     const int wb = VB::wblk(vb) * 64;
 #pragma unroll
     for (int i = 0; i < WDMA; ++i) {
-      const _Float16* src = t < 9 ? wsrc[i] + t * KW + wb : dsrc[i] + wb;
+      const _Float16* src = t < 9 ? wsrc[i] + t * kin + wb : dsrc[i] + wb;
       xdma16(src, wring + (s % NSLOT) * WB + (i * NW + wid) * 1024);
     }
   };
@@ -278,7 +287,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + PD < NSTEPS) dma_w(S + PD);
     if constexpr (CB + 1 < NBLK && S == plan.ps(CB + 1)) dma_patch(CB + 1, (CB + 1) & 1);
-    if constexpr (TPW == 1 && S == plan.rs) {
+    if constexpr (TPW == 1 && S == plan.rs && !PART) {
       __builtin_amdgcn_sched_barrier(0);
       load_epi();
     }
@@ -294,6 +303,26 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   });
   if constexpr (DBG == 4) trace_stamp(a.trace, 2);
   xwait_vm<0>();
+  if constexpr (PART > 0) {  // f32 partials of both: acc / accd[tm][tn] = 4 consecutive channels of one pixel
+    const size_t plane = (size_t)a.B * H * W * Cout;
+    float* __restrict__ pt = a.part + blockIdx.y * plane;
+    float* __restrict__ pd = a.part + (PART + blockIdx.y) * plane;
+    int th0, tw0;
+    tile_origin(0, th0, tw0);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int m = wm * WTM + tm * 16 + o;
+      const int y = m / TW, x = m - (m / TW) * TW;
+      const size_t pixo = (((size_t)img * H + th0 + y) * W + tw0 + x) * Cout + n0 + wn * WTN + q * 8;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const size_t e = pixo + (tn >> 1) * 32 + (tn & 1) * 4;
+        *reinterpret_cast<f32x4*>(pt + e) = acc[tm][tn];
+        *reinterpret_cast<f32x4*>(pd + e) = accd[tm][tn];
+      }
+    }
+    return;
+  }
   epilogue(TPW - 1);
   if constexpr (DBG == 4) {
     trace_stamp(a.trace, 3);
@@ -318,6 +347,20 @@ static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
   const int x = xg && nsp % 8 == 0;
   hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT, X3, DBG, TPW>), dim3(nsp * ntn),
                      dim3(WM * WN * 64), 0, s, a, x);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+// split-K partial launch (PART = NS): grid.y = NS splits of CIN channels, f32 partials to a.part
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int NS>
+static int run_s2x_part(const ConvS2Args& a, hipStream_t s) {
+  PA_CHECK(a.part && a.Cin == NS * CIN && a.Hin == 2 * a.Hout && a.Win == 2 * a.Wout && a.Hout % TH == 0 &&
+               a.Wout % TW == 0 && a.Cout % BN == 0,
+           "s2x split-K: Cin %d Cout %d %dx%d", a.Cin, a.Cout, a.Hout, a.Wout);
+  const int ntn = a.Cout / BN;
+  const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW);
+  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, 1, true, false, 0, 1, NS>), dim3(nsp * ntn, NS),
+                     dim3(WM * WN * 64), 0, s, a, 0);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

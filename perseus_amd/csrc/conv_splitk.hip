@@ -1,0 +1,121 @@
+// Split-K form of layers 2-4's convs for batches of a few frames (the streaming pose stage:
+// one frame per camera per tick, SURVEY.md 8 configs[4]).
+//
+// At B = 3 the batched kernels (conv_gx.h, conv_s2x.h) give most CUs nothing to do: layer3
+// runs 12 workgroups of a 36-step K loop, layer4 16 of 72 steps, so a launch takes as long
+// as one workgroup's whole K loop (16-18 us) while the chip idles.  Here the K loop is cut
+// into a.Cin / 64 splits of 9 steps (10 for a stride-2 entry: 9 taps + the downsample),
+// grid.y = split, every split writes its f32 accumulators to a partial map, and
+// splitk_reduce sums the splits in a fixed order (deterministic: same input, same bits) and
+// applies the batched kernels' epilogue -- bias, residual, ReLU of models.py's BasicBlock
+// convs (torchvision resnet18 via models.py:6-40).
+//
+// Opt-in per handle (pa_detector_set_split_k): the sum order differs from the
+// single-pass kernels', so a split-K forward is not bit-identical to the batched one
+// (both are within the fp16 path's error budget).
+#include "conv_s2x.h"
+
+namespace pa {
+
+// out[p][c] = relu(sum_s part[s][p][c] + bias[c] (+ res[p][c])), 8 channels per thread,
+// splits summed in order 0 .. nsplit-1.  With out2 (a stride-2 entry's downsample), the
+// threads past n / 8 reduce the second partial set part[nsplit ..] into
+// out2[p][c] = sum_s + bias2[c] (no ReLU).
+__global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ part, int nsplit, unsigned n,
+                                                     const float* __restrict__ bias, const _Float16* __restrict__ res,
+                                                     _Float16* __restrict__ out, int Cout, const float* __restrict__ bias2,
+                                                     _Float16* __restrict__ out2) {
+  unsigned e = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const bool second = e >= n;
+  if (second) {
+    e -= n;
+    if (!out2 || e >= n) return;
+    part += (size_t)nsplit * n;
+    bias = bias2;
+    out = out2;
+    res = nullptr;
+  }
+  const int c = (int)(e % (unsigned)Cout);
+  f32x4 lo = *reinterpret_cast<const f32x4*>(part + e), hi = *reinterpret_cast<const f32x4*>(part + e + 4);
+  for (int s = 1; s < nsplit; ++s) {
+    lo += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e);
+    hi += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e + 4);
+  }
+  // the batched epilogue's order: (acc + bias) (+ res), then ReLU
+  lo += *reinterpret_cast<const f32x4*>(bias + c);
+  hi += *reinterpret_cast<const f32x4*>(bias + c + 4);
+  half8 r{};
+  if (res) r = *reinterpret_cast<const half8*>(res + e);
+  half8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float v0 = lo[j], v1 = hi[j];
+    if (res) {
+      v0 += (float)r[j];
+      v1 += (float)r[j + 4];
+    }
+    o[j] = (_Float16)(second ? v0 : fmaxf(v0, 0.f));
+    o[j + 4] = (_Float16)(second ? v1 : fmaxf(v1, 0.f));
+  }
+  *reinterpret_cast<half8*>(out + e) = o;
+}
+
+static int launch_reduce(const float* part, int nsplit, size_t n, const float* bias, const _Float16* res, _Float16* out,
+                         int Cout, const float* bias2, _Float16* out2, hipStream_t s) {
+  PA_CHECK(n % 8 == 0 && n < 0x40000000u && Cout % 8 == 0, "split-K reduce: %zu elements", n);
+  const size_t threads = (out2 ? 2 * n : n) / 8;
+  hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, part, nsplit, (unsigned)n, bias,
+                     res, out, Cout, bias2, out2);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+size_t splitk_part_floats(int B) {
+  // per frame, nsplit * H * W * Cout is 2*32*32*128 = 4*16*16*256 = 8*8*8*512 = 262144 for every
+  // stride-1 conv, and 2 maps * nsplit * H * W * Cout = 2*4*8*8*512 the same for layer4's entry
+  return (size_t)B * 262144;
+}
+
+int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s) {
+  PA_CHECK(a.stride == 1 && a.pad == 1 && (a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES)),
+           "split-K conv: stride-1, relu (+residual) only (epi %d)", a.epi);
+  PA_CHECK(a.B <= 64, "split-K conv: batch %d above 64", a.B);
+  if (a.B <= 0) return PA_OK;
+  int rc;
+  if (a.Cin == 128 && a.Cout == 128 && a.Hout == 32 && a.Wout == 32)
+    rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 2>(a, s);
+  else if (a.Cin == 256 && a.Cout == 256 && a.Hout == 16 && a.Wout == 16)
+    rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 4>(a, s);
+  else if (a.Cin == 512 && a.Cout == 512 && a.Hout == 8 && a.Wout == 8)
+    rc = run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8>(a, s);
+  else {
+    set_error("split-K conv: no configuration for %dx%d x %d -> %d", a.Hout, a.Wout, a.Cin, a.Cout);
+    return PA_EINVAL;
+  }
+  if (rc != PA_OK) return rc;
+  return launch_reduce(a.part, a.Cin / 64, (size_t)a.B * a.Hout * a.Wout * a.Cout, a.bias,
+                       (const _Float16*)((a.epi & EPI_RES) ? a.res : nullptr), (_Float16*)a.out, a.Cout, nullptr, nullptr, s);
+}
+
+int launch_conv3x3s2_small(const ConvS2Args& a, hipStream_t s, const char** kname) {
+  PA_CHECK(a.B <= 64, "split-K conv: batch %d above 64", a.B);
+  if (a.B <= 0) return PA_OK;
+  if (a.Hout == 32 && a.Cin == 64 && a.Cout == 128) {
+    // one input-channel block, nothing to split: one 4x16 tile per workgroup (B = 3: 96
+    // workgroups of 10 steps, 6.5 us; the batched kernel runs 12 workgroups of 4 tiles, 40
+    // steps, 17.8 us)
+    if (kname) *kname = "conv3x3s2x_l2_small";
+    return run_s2x<4, 16, 64, 2, 2, 64, 3>(a, false, s);
+  }
+  if (a.Hout == 8 && a.Cin == 256 && a.Cout == 512) {
+    if (kname) *kname = "conv3x3s2x_l4_splitk";
+    const int rc = run_s2x_part<8, 8, 64, 2, 2, 64, 3, 4>(a, s);
+    if (rc != PA_OK) return rc;
+    return launch_reduce(a.part, 4, (size_t)a.B * 64 * 512, a.bias, nullptr, (_Float16*)a.out, 512, a.bias2,
+                         (_Float16*)a.out2, s);
+  }
+  set_error("s2x small batch: no configuration for %dx%d x %d -> %d", a.Hout, a.Wout, a.Cin, a.Cout);
+  return PA_EINVAL;
+}
+
+}  // namespace pa

@@ -60,6 +60,8 @@ struct pa_detector {
   int device = 0;
   int variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // pa_detector_debug_set_variant (0 = shipped)
   unsigned long long* trace = nullptr;         // pa_detector_debug_set_trace
+  int splitk_max = 0;                          // pa_detector_set_split_k: batches <= this run split-K
+  float* part = nullptr;                       // its f32 partials (splitk_part_floats(splitk_max))
 };
 
 namespace pa {
@@ -333,6 +335,19 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   int hw = 64;
   int launch = 1;  // stem = 0
   auto trace = [&]() { return g_trace ? g_trace + (size_t)TRACE_LAUNCH * launch++ : nullptr; };
+  // stride-1 convs: split-K form for small batches (pa_detector_set_split_k, conv_splitk.hip)
+  auto conv_s1 = [&](ConvArgs& a, const char** kn) -> int {
+    if constexpr (std::is_same<T, _Float16>::value) {
+      const int layer = a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : a.Hout == 8 ? 4 : 0;
+      if (layer && B <= d->splitk_max && g_variant[layer] == 0 && !(a.epi & EPI_HEAD)) {
+        static const char* names[5] = {"", "", "conv3x3x_l2_splitk", "conv3x3x_l3_splitk", "conv3x3x_l4_splitk"};
+        *kn = names[layer];
+        a.part = d->part;
+        return launch_conv3x3_splitk(a, s);
+      }
+    }
+    return launch_conv3x3_s1<T>(a, s, kn);
+  };
   for (const Block& b : d->blocks) {
     const ConvL& c1 = d->convs[b.conv1];
     const ConvL& c2 = d->convs[b.conv2];
@@ -366,7 +381,14 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       sa.Wout = ho;
       sa.Cout = c1.cout;
       sa.trace = trace();
-      PA_RUN(launch_conv3x3s2_ds<T>(sa, s, &kn), kn);
+      bool small = false;
+      if constexpr (std::is_same<T, _Float16>::value) small = B <= d->splitk_max && g_variant[6] == 0 && ho != 16;
+      if (small) {
+        sa.part = d->part;
+        PA_RUN(launch_conv3x3s2_small(sa, s, &kn), kn);
+      } else {
+        PA_RUN(launch_conv3x3s2_ds<T>(sa, s, &kn), kn);
+      }
       res = D;
       out = D;
     } else {
@@ -383,7 +405,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       a.epi = EPI_RELU;
       a.trace = trace();
       if (c1.stride == 1)
-        PA_RUN(launch_conv3x3_s1<T>(a, s, &kn), kn);
+        PA_RUN(conv_s1(a, &kn), kn);
       else
         PA_RUN(launch_conv<T>(a, 3, s, &kn), kn);
       if (b.ds >= 0) {
@@ -426,7 +448,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       b2.fcb = d->fcb;
       b2.y = y;
     }
-    PA_RUN(launch_conv3x3_s1<T>(b2, s, &kn), kn);
+    PA_RUN(conv_s1(b2, &kn), kn);
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
   }
@@ -648,6 +670,7 @@ void pa_detector_destroy(pa_detector* d) {
   if (d->ws) hipFree(d->ws);
   if (d->pool) hipFree(d->pool);
   if (d->cnt) hipFree(d->cnt);
+  if (d->part) hipFree(d->part);
   delete d;
 }
 
@@ -655,6 +678,24 @@ int pa_detector_reserve(pa_detector* d, int max_batch) {
   PA_CHECK(d && max_batch >= 0, "bad arguments");
   // forward / forward_rgbd never use more than one chunk's workspace
   return pa::ensure_ws(d, max_batch < pa::kChunk ? max_batch : pa::kChunk);
+}
+
+int pa_detector_set_split_k(pa_detector* d, int max_batch) {
+  PA_CHECK(d, "null detector");
+  PA_CHECK(max_batch >= 0 && max_batch <= 64, "split-K max batch %d not in [0,64]", max_batch);
+  if (max_batch > d->splitk_max || max_batch == 0) {
+    if (d->part) PA_HIP(hipFree(d->part));
+    d->part = nullptr;
+    d->splitk_max = 0;
+    if (max_batch == 0) return PA_OK;
+    if (hipMalloc(&d->part, pa::splitk_part_floats(max_batch) * sizeof(float)) != hipSuccess) {
+      (void)hipGetLastError();
+      pa::set_error("split-K partials: hipMalloc failed");
+      return PA_ENOMEM;
+    }
+  }
+  d->splitk_max = max_batch;
+  return PA_OK;
 }
 
 int pa_detector_set_precision(pa_detector* d, int precision) {

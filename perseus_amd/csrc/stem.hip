@@ -556,6 +556,10 @@ int launch_stem_pool_rgbd(const RgbdSrc& src, int B, const _Float16* w, const fl
   PA_CHECK(src.rgb && src.depth, "stem rgbd: null frame pointer");
   PA_CHECK(src.Hs >= 256 && src.Ws >= 256, "stem rgbd: source %dx%d smaller than 256x256", src.Hs, src.Ws);
   if (B <= 0) return PA_OK;
+  // a few frames (the streaming batch): shorter bands, so the grid still covers the chip
+  // (B = 3: 96 workgroups of 2 pooled rows instead of 12 of 16; same arithmetic per row)
+  if (B <= 8) return run_stem4<2, 2, true>(nullptr, B, 4, w, bias, out, s, src);
+  if (B <= 24) return run_stem4<4, 2, true>(nullptr, B, 4, w, bias, out, s, src);
   return run_stem4<16, 2, true>(nullptr, B, 4, w, bias, out, s, src);
 }
 
@@ -585,6 +589,9 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     // prefetch depth 3 / 4 measured 29.7 / 30.4 us)
     default: break;
   }
+  // small batches: shorter bands (as launch_stem_pool_rgbd)
+  if (B <= 8) return run_stem4<2, 2>(x, B, Cin, w, bias, out, s);
+  if (B <= 24) return run_stem4<4, 2>(x, B, Cin, w, bias, out, s);
   return run_stem4<16, 2>(x, B, Cin, w, bias, out, s);  // also variants 14 / 24 without a trace buffer
 }
 

@@ -111,6 +111,7 @@ class KeypointCNN(nn.Module):
         self._handle_dev = None
         self._stamp = None
         self._variants = {}
+        self._split_k = 0
         self.eval()
 
     # -------------------------------------------------------------- weights
@@ -139,6 +140,8 @@ class KeypointCNN(nn.Module):
                                             self.H, self.W, _lib.C.byref(h)), "pa_detector_create")
         for layer in range(8):
             _lib.check(L.pa_detector_debug_set_variant(h, layer, self._variants.get(layer, 0)), "set_variant")
+        if self._split_k:
+            _lib.check(L.pa_detector_set_split_k(h, self._split_k), "set_split_k")
         return h
 
     def _ensure_handle(self, device: torch.device):
@@ -168,6 +171,16 @@ class KeypointCNN(nn.Module):
             for layer in range(8):
                 _lib.check(L.pa_detector_debug_set_variant(self._handle, layer, self._variants.get(layer, 0)),
                            "set_variant")
+
+    def set_split_k(self, max_batch: int) -> None:
+        """Latency mode (pa_detector_set_split_k): fp16 forwards of at most `max_batch`
+        frames run layers 2-4's stride-1 convs split-K (fills the chip at a few frames;
+        deterministic, not bit-identical to the batched kernels).  0 turns it off."""
+        if not 0 <= max_batch <= 64:
+            raise ValueError(f"split-K max batch {max_batch} not in [0, 64]")
+        self._split_k = int(max_batch)
+        if self._handle is not None:
+            _lib.check(_lib.lib().pa_detector_set_split_k(self._handle, self._split_k), "set_split_k")
 
     def set_trace(self, trace: "torch.Tensor | None") -> None:
         """Timestamp buffer of the tracing kernel variants (None = off)."""

