@@ -329,7 +329,7 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pos
              "device_ms_per_tick": round(e0.elapsed_time(e1) / 20, 4)}
         if mode == "pose":
             r["window_frames"] = window
-            r["stage"] = ("forward_rgbd + postprocess + pa_window_advance + pa_trajectory_linearize + "
+            r["stage"] = ("forward_rgbd_px (split-K latency mode) + pa_window_advance + pa_trajectory_linearize + "
                           "pa_trajectory_gn_step + pa_window_retract")
             r["solved_last_tick"] = int((pipe.info_h.numpy() == 0).sum())
         res[mode] = r

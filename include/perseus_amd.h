@@ -88,6 +88,13 @@ int pa_detector_forward(pa_detector* d, const float* x_dev, int B, float* y_dev,
 int pa_detector_forward_rgbd(pa_detector* d, const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws,
                              int bgr, float near_m, float far_m, float* y_dev, void* stream);
 
+/* pa_detector_forward_rgbd + pa_keypoints_postprocess (no target) in the same launches:
+ * the head also writes the pixel coordinates px (B, n_kp, 2) f32, kornia's denormalize
+ * (streaming.py:128-131), bit-identical to the separate postprocess.  The streaming
+ * tick's detector call (one launch fewer per tick). */
+int pa_detector_forward_rgbd_px(pa_detector* d, const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws,
+                                int bgr, float near_m, float far_m, float* y_dev, float* px_dev, void* stream);
+
 /* Same forward with a HIP event after every kernel: writes up to max_n per-kernel
  * durations (ms) into ms_out and their names into names_out (may be NULL), returns
  * the number of kernels or <0.  Synchronises the stream (diagnostics only). */

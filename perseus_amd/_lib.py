@@ -60,6 +60,8 @@ _SIGS = {
                                            C.c_void_p, C.c_void_p, C.c_void_p]),
     "pa_detector_forward_rgbd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                            C.c_float, C.c_float, C.c_void_p, C.c_void_p]),
+    "pa_detector_forward_rgbd_px": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                              C.c_float, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p]),
     "pa_trajectory_gn_workspace": (C.c_size_t, [C.c_int, C.c_int]),
     "pa_trajectory_gn_step": (C.c_int, [C.c_int, C.c_int, C.c_int] + [C.c_void_p] * 11 + [C.c_double]
                               + [C.c_void_p] * 6 + [C.c_size_t, C.c_void_p]),

@@ -139,9 +139,10 @@ int launch_head_x3(const _Float16* in, int B, int HW, int C, const float* fcw, c
 template <typename T>
 int launch_maxpool(const T* in, int B, int H, int W, int C, T* out, hipStream_t s);
 
+// px (optional): also the keypoints denormalized to an H x W image (launch_postprocess's values)
 template <typename T>
 int launch_head(const T* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
-                hipStream_t s);
+                hipStream_t s, float* px = nullptr, int H = 0, int W = 0);
 
 int launch_preprocess(const uint8_t* rgb, const float* depth, int B, int Hs, int Ws, int bgr, float near_m,
                       float far_m, int H, int W, float* x, hipStream_t s);

@@ -519,9 +519,12 @@ __global__ __launch_bounds__(256) void head_kernel(const T* __restrict__ in, int
 // order, with every load (16 pixels per thread, the thread's fc weights) issued
 // before the first add.  head_kernel's runtime-length fc loop waits for each
 // output's weights in turn (~10 us per batch-64 launch).
+// px (optional): the keypoints also denormalized to pixels (postprocess_kernel's
+// arithmetic, the streaming tick's output) by the threads that write y
 template <int NOUT>
 __global__ __launch_bounds__(256) void head_fp16(const _Float16* __restrict__ in, const float* __restrict__ fcw,
-                                                 const float* __restrict__ fcb, float* __restrict__ y) {
+                                                 const float* __restrict__ fcb, float* __restrict__ y,
+                                                 float* __restrict__ px, int H, int W) {
   constexpr int HW = 64, C = 512;
   __shared__ float csum[4][C];
   __shared__ float part[4][NOUT];
@@ -558,7 +561,11 @@ __global__ __launch_bounds__(256) void head_fp16(const _Float16* __restrict__ in
     if (lane == 0) part[wid][j] = v;
   }
   __syncthreads();
-  if (tid < NOUT) y[(size_t)n * NOUT + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + fcb[tid];
+  if (tid < NOUT) {
+    const float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + fcb[tid];
+    y[(size_t)n * NOUT + tid] = v;
+    if (px) px[(size_t)n * NOUT + tid] = kornia_denorm(v, (tid & 1) ? H : W);
+  }
 }
 
 // fp16x3 parity mode: head_fp16's arithmetic on the f32 values hi + lo of the layer4
@@ -626,19 +633,19 @@ int launch_head_x3(const _Float16* in, int B, int HW, int C, const float* fcw, c
 
 template <typename T>
 int launch_head(const T* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
-                hipStream_t s) {
+                hipStream_t s, float* px, int H, int W) {
   PA_CHECK(C == 512 && nout <= 32, "head: C=%d nout=%d", C, nout);  // 4 pixel groups x 64 chunks
   if (B <= 0) return PA_OK;
   if constexpr (std::is_same<T, _Float16>::value) {
     if (HW == 64 && nout == 16 && g_variant[7] != 1) {  // 1: the generic head_kernel
-      hipLaunchKernelGGL(head_fp16<16>, dim3(B), dim3(256), 0, s, in, fcw, fcb, y);
+      hipLaunchKernelGGL(head_fp16<16>, dim3(B), dim3(256), 0, s, in, fcw, fcb, y, px, H, W);
       PA_LAUNCH_CHECK();
       return PA_OK;
     }
   }
   hipLaunchKernelGGL(head_kernel<T>, dim3(B), dim3(256), 0, s, in, HW, C, fcw, fcb, nout, y);
   PA_LAUNCH_CHECK();
-  return PA_OK;
+  return px ? launch_postprocess(y, nullptr, B, nout / 2, H, W, px, nullptr, s) : PA_OK;
 }
 
 // ------------------------------------------------------ pre/post-processing
@@ -718,8 +725,7 @@ template int launch_stem<_Float16>(const float*, int, int, const _Float16*, cons
 template int launch_stem<float>(const float*, int, int, const float*, const float*, float*, hipStream_t);
 template int launch_maxpool<_Float16>(const _Float16*, int, int, int, int, _Float16*, hipStream_t);
 template int launch_maxpool<float>(const float*, int, int, int, int, float*, hipStream_t);
-template int launch_head<_Float16>(const _Float16*, int, int, int, const float*, const float*, int, float*,
-                                   hipStream_t);
-template int launch_head<float>(const float*, int, int, int, const float*, const float*, int, float*, hipStream_t);
+template int launch_head<_Float16>(const _Float16*, int, int, int, const float*, const float*, int, float*, hipStream_t, float*, int, int);
+template int launch_head<float>(const float*, int, int, int, const float*, const float*, int, float*, hipStream_t, float*, int, int);
 
 }  // namespace pa

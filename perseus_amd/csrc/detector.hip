@@ -305,7 +305,7 @@ struct Prof {
 
 template <typename T>
 static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof,
-                     const RgbdSrc* rgbd = nullptr) {
+                     const RgbdSrc* rgbd = nullptr, float* px = nullptr) {
   const T* wts = std::is_same<T, float>::value ? (const T*)d->w32 : (const T*)d->w16;
   T* S = reinterpret_cast<T*>(d->ws);
   const size_t stem_el = stem_elems(B, d->prec);
@@ -452,7 +452,10 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
   }
-  if (!fuse_head) PA_RUN(launch_head<T>(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s), "avgpool_fc");
+  if (!fuse_head)
+    PA_RUN(launch_head<T>(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s, px, d->H, d->W), "avgpool_fc");
+  else if (px)
+    PA_RUN(launch_postprocess(y, nullptr, B, d->n_kp, d->H, d->W, px, nullptr, s), "postprocess");
   return PA_OK;
 }
 
@@ -590,7 +593,7 @@ static int forward(pa_detector* d, const float* x, int B, float* y, hipStream_t 
 }
 
 // camera frames -> keypoints, preprocess fused into the stem (fp16, 4-channel models)
-static int forward_rgbd(pa_detector* d, const RgbdSrc& src, int B, float* y, hipStream_t s) {
+static int forward_rgbd(pa_detector* d, const RgbdSrc& src, int B, float* y, hipStream_t s, float* px = nullptr) {
   PA_CHECK(d, "null detector");
   PA_CHECK(B >= 0, "batch %d", B);
   if (B == 0) return PA_OK;
@@ -607,7 +610,8 @@ static int forward_rgbd(pa_detector* d, const RgbdSrc& src, int B, float* y, hip
     RgbdSrc c = src;
     c.rgb = src.rgb + off * frame * 3;
     c.depth = src.depth + off * frame;
-    const int rc = forward_t<_Float16>(d, nullptr, nb, y + off * 2 * (size_t)d->n_kp, s, nullptr, &c);
+    const int rc = forward_t<_Float16>(d, nullptr, nb, y + off * 2 * (size_t)d->n_kp, s, nullptr, &c,
+                                       px ? px + off * 2 * (size_t)d->n_kp : nullptr);
     if (rc != PA_OK) return rc;
   }
   return PA_OK;
@@ -621,6 +625,13 @@ int pa_detector_forward_rgbd(pa_detector* d, const uint8_t* rgb_dev, const float
                              int bgr, float near_m, float far_m, float* y_dev, void* stream) {
   const pa::RgbdSrc src{rgb_dev, depth_dev, Hs, Ws, bgr, near_m, far_m};
   return pa::forward_rgbd(d, src, B, y_dev, (hipStream_t)stream);
+}
+
+int pa_detector_forward_rgbd_px(pa_detector* d, const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws,
+                                int bgr, float near_m, float far_m, float* y_dev, float* px_dev, void* stream) {
+  PA_CHECK(px_dev, "forward_rgbd_px: null pixel output");
+  const pa::RgbdSrc src{rgb_dev, depth_dev, Hs, Ws, bgr, near_m, far_m};
+  return pa::forward_rgbd(d, src, B, y_dev, (hipStream_t)stream, px_dev);
 }
 
 const char* pa_last_error(void) { return pa::g_err.c_str(); }

@@ -324,15 +324,40 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
     if constexpr (PRE) {
       const int r0 = src.Hs / 2 - 128, c0 = src.Ws / 2 - 128;
       const size_t row = ((size_t)n * src.Hs + hi + r0) * src.Ws + c0 + lcg * 4;
-      const int cr = src.bgr ? 2 : 0, cb = src.bgr ? 0 : 2;
+      // the 4 pixels' 12 bytes as 3 dwords and their depths as one float4 when aligned (the
+      // centre crop of a 4-aligned width always is)
+      uint8_t px[12];
+      float dp[4];
+      const uint8_t* p8 = src.rgb + row * 3;
+      if ((((uintptr_t)p8) & 3) == 0 && (((uintptr_t)(src.depth + row)) & 15) == 0) {
+        const uint32_t* p32 = reinterpret_cast<const uint32_t*>(p8);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const uint32_t wv = p32[j];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) px[4 * j + b] = (uint8_t)(wv >> (8 * b));
+        }
+        const float4 d4 = *reinterpret_cast<const float4*>(src.depth + row);
+        dp[0] = d4.x;
+        dp[1] = d4.y;
+        dp[2] = d4.z;
+        dp[3] = d4.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) px[j] = p8[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dp[k] = src.depth[row + k];
+      }
       float a[4][4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint8_t* px = src.rgb + (row + k) * 3;
-        a[0][k] = (float)((double)px[cr] / 255.0);  // numpy f64 /255 then .float()
-        a[1][k] = (float)((double)px[1] / 255.0);
-        a[2][k] = (float)((double)px[cb] / 255.0);
-        float d = src.depth[row + k];
+        // numpy's f64 / 255 then .float(): the correctly rounded f32 quotient is the same
+        // value for every byte (checked exhaustively, tests/test_preprocess.py)
+        const float c0 = (float)px[3 * k], c2 = (float)px[3 * k + 2];  // constant indices: no scratch array
+        a[0][k] = (src.bgr ? c2 : c0) / 255.0f;
+        a[1][k] = (float)px[3 * k + 1] / 255.0f;
+        a[2][k] = (src.bgr ? c0 : c2) / 255.0f;
+        float d = dp[k];
         if (isnan(d) || isinf(d)) d = 0.f;
         d = d / 0.035f;  // streaming.py:76
         if (src.near_m >= 0.f || src.far_m >= 0.f) {

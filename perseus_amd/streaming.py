@@ -12,9 +12,10 @@ its optimizer live in downstream GTSAM code, so this build defines the loop: one
 Gauss-Newton step per tick.  Per tick:
 
   host: frames -> pinned staging (centre crop rows only, or the full frame)
-  GPU (one hipGraph replay on a private stream): H2D -> pa_detector_forward_rgbd
-       (B = n_cams; the preprocess runs inside the stem's row loads; fp32: pa_preprocess_rgbd
-       + pa_detector_forward) -> pa_keypoints_postprocess -> D2H pixels
+  GPU (one hipGraph replay on a private stream): H2D -> pa_detector_forward_rgbd_px
+       (B = n_cams; the preprocess runs inside the stem's row loads, the denormalize in the
+       head; fp32: pa_preprocess_rgbd + pa_detector_forward + pa_keypoints_postprocess) -> D2H
+       pixels
        [pose stage] -> pa_window_advance (window shifts one frame, the new keypoints
        appended, the new pose predicted by the dynamics model) -> pa_trajectory_linearize
        (whitened factors of every camera's window) -> pa_trajectory_gn_step ->
@@ -115,12 +116,12 @@ class StreamingPipeline:
                                             int(self.bgr), self.near, self.far, self.H, self.W, self.x.data_ptr(), s),
                        "preprocess")
             _lib.check(L.pa_detector_forward(self._h, self.x.data_ptr(), self.n, self.y.data_ptr(), s), "forward")
-        else:  # fp16: the preprocess runs inside the stem's row loads
-            _lib.check(L.pa_detector_forward_rgbd(self._h, self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n,
-                                                  self.sh, self.sw, int(self.bgr), self.near, self.far,
-                                                  self.y.data_ptr(), s), "forward_rgbd")
-        _lib.check(L.pa_keypoints_postprocess(self.y.data_ptr(), None, self.n, self.model.n_keypoints, self.H, self.W,
-                                              self.px_d.data_ptr(), None, s), "postprocess")
+            _lib.check(L.pa_keypoints_postprocess(self.y.data_ptr(), None, self.n, self.model.n_keypoints, self.H,
+                                                  self.W, self.px_d.data_ptr(), None, s), "postprocess")
+        else:  # fp16: the preprocess runs inside the stem's row loads, the denormalize in the head
+            _lib.check(L.pa_detector_forward_rgbd_px(self._h, self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n,
+                                                     self.sh, self.sw, int(self.bgr), self.near, self.far,
+                                                     self.y.data_ptr(), self.px_d.data_ptr(), s), "forward_rgbd_px")
         self.px_h.copy_(self.px_d, non_blocking=True)
         if self.pose_L:  # the pose stage, all on this stream (HBM-resident window)
             pipeline.window_advance(self.y, self.win, dt=self.dt, vel_frame=self.vel_frame)

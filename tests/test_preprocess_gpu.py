@@ -92,3 +92,25 @@ def test_stem_fused_preprocess_fp32_and_errors():
     with pytest.raises(RuntimeError):
         m.forward_rgbd(rgb.float(), depth)
     assert isinstance(_lib.lib().pa_last_error(), bytes)
+
+
+@pytest.mark.parametrize("split_k", [0, 8])
+def test_forward_rgbd_px_fuses_postprocess(split_k):
+    """pa_detector_forward_rgbd_px (the streaming tick's call): the same keypoints as
+    pa_detector_forward_rgbd, and pixels bit-identical to pa_keypoints_postprocess of them
+    (the denormalize runs in the head), in both the batched and the split-K latency mode."""
+    from perseus_amd import _lib
+    from perseus_amd.detector import denormalize_pixel_coordinates
+
+    m = _model()
+    m.set_split_k(split_k)
+    rgb, depth = _frames(7, 3, 720, 1280)
+    ref = m.forward_rgbd(rgb, depth)
+    h = m._ensure_handle(rgb.device)
+    y = torch.empty_like(ref)
+    px = torch.full((3, 8, 2), float("nan"), device=rgb.device)
+    _lib.check(_lib.lib().pa_detector_forward_rgbd_px(h, rgb.data_ptr(), depth.data_ptr(), 3, 720, 1280, 1, -1.0, -1.0,
+                                                       y.data_ptr(), px.data_ptr(), _lib.stream_of(rgb.device)),
+               "forward_rgbd_px")
+    assert torch.equal(y, ref)
+    assert torch.equal(px, denormalize_pixel_coordinates(ref))
