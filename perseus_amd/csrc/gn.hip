@@ -38,6 +38,7 @@ struct GnArgs {
   int32_t* info;
   double* ws;
   unsigned long long* trace;  // timing only (pa_debug_gn_set_trace): 256 s_memrealtime stamps per trajectory
+  int zero_each;              // gn_twisted_kernel: re-zero the assembly staging every frame (A/B only)
 };
 
 // slot s of trajectory t's trace (lane 0 of the calling wave only)
@@ -144,9 +145,18 @@ __device__ __forceinline__ void gn_load_frame(const GnArgs& a, long f, GnFrameLo
   }
 }
 
-template <int RP>
+template <int RP, bool ZERO = true>
 __device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const GnFrameLoads<RP>& ld, GnStage<RP>& st,
                                                double* blk);
+
+// the staging zeroed once (the pad rows and every position no factor writes stay zero;
+// gn_build_frame<RP, false> then writes only the factor positions, zeros included)
+template <int RP>
+__device__ __forceinline__ void gn_zero_stage(GnStage<RP>& st) {
+  const int lane = threadIdx.x & 63;
+  for (int e = lane; e < (int)(sizeof(GnStage<RP>) / sizeof(double)); e += 64) (&st.AT[0][0])[e] = 0.0;
+  wave_order();
+}
 
 template <int RP>
 __device__ __forceinline__ void gn_assemble_frame(const GnArgs& a, long f, GnStage<RP>& st, double* blk) {
@@ -155,7 +165,7 @@ __device__ __forceinline__ void gn_assemble_frame(const GnArgs& a, long f, GnSta
   gn_build_frame<RP>(a, f, ld, st, blk);
 }
 
-template <int RP>
+template <int RP, bool ZERO>
 __device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const GnFrameLoads<RP>& ld, GnStage<RP>& st,
                                                double* blk) {
   using namespace gn;
@@ -175,14 +185,18 @@ __device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const Gn
   const int(&js)[JR] = ld.js;
   const double rv = ld.rv, n0 = ld.n0, n3 = ld.n3, n1 = ld.n1, n2 = ld.n2, p3 = ld.p3;
   const int rs = ld.rs;
-  // ---- staging: zero, then fill (one wave: its LDS ops run in order)
-  for (int e = lane; e < NV * RPP; e += 64) (&AT[0][0])[e] = 0.0;
-  for (int e = lane; e < NV * 12; e += 64) {
-    (&ANT[0][0])[e] = 0.0;
-    (&BT[0][0])[e] = 0.0;
+  // ---- staging: zero (ZERO; else once per launch, gn_zero_stage), then fill (one wave: its LDS
+  // ops run in order).  Without the per-frame zeroing every factor position is written, with
+  // 0 for a missing neighbour pair (first / last frame)
+  if constexpr (ZERO) {
+    for (int e = lane; e < NV * RPP; e += 64) (&AT[0][0])[e] = 0.0;
+    for (int e = lane; e < NV * 12; e += 64) {
+      (&ANT[0][0])[e] = 0.0;
+      (&BT[0][0])[e] = 0.0;
+    }
+    for (int e = lane; e < RPP; e += 64) rT[e] = 0.0;
+    wave_order();
   }
-  for (int e = lane; e < RPP; e += 64) rT[e] = 0.0;
-  wave_order();
   // projections: rows 2k, 2k + 1; J column-major 2 x 6
 #pragma unroll
   for (int q = 0; q < JR; ++q) {
@@ -194,40 +208,42 @@ __device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const Gn
   }
   if (vr) rT[lane] = rs == 0 ? rv : 0.0;
   const int rn = 2 * K, rp = rn + 9;  // first row of the (l, l+1) / (l-1, l) blocks
-  if (nxt) {
+  if (nxt || !ZERO) {
+    const double m0 = nxt ? n0 : 0.0, m3 = nxt ? n3 : 0.0, m1 = nxt ? n1 : 0.0, m2 = nxt ? n2 : 0.0;
     if (lane < 36) {  // dynamics: 6 x 6 / 6 x 3 / 6 x 3, column-major
       const int c = lane / 6, row = lane - c * 6;
-      AT[c][rn + row] = n0;
-      ANT[c][row] = n0;
-      BT[c][row] = n3;
+      AT[c][rn + row] = m0;
+      ANT[c][row] = m0;
+      BT[c][row] = m3;
       if (lane < 18) {
-        AT[6 + c][rn + row] = n1;
-        ANT[6 + c][row] = n1;
-        AT[9 + c][rn + row] = n2;
-        ANT[9 + c][row] = n2;
+        AT[6 + c][rn + row] = m1;
+        ANT[6 + c][row] = m1;
+        AT[9 + c][rn + row] = m2;
+        ANT[9 + c][row] = m2;
       }
     } else if (lane < 45) {  // const velocity: 3 x 3 on the velocity block
       const int e = lane - 36, c = e / 3, row = e - c * 3;
-      AT[9 + c][rn + 6 + row] = n0;
-      ANT[9 + c][6 + row] = n0;
-      BT[9 + c][6 + row] = n3;
+      AT[9 + c][rn + 6 + row] = m0;
+      ANT[9 + c][6 + row] = m0;
+      BT[9 + c][6 + row] = m3;
     } else if (lane < 51) {
-      rT[rn + lane - 45] = n0;
+      rT[rn + lane - 45] = m0;
     } else if (lane < 54) {
-      rT[rn + 6 + lane - 51] = n0;
+      rT[rn + 6 + lane - 51] = m0;
     }
   }
-  if (prv) {
+  if (prv || !ZERO) {
+    const double q3 = prv ? p3 : 0.0;
     if (lane < 36) {
       const int c = lane / 6, row = lane - c * 6;
-      AT[c][rp + row] = p3;
+      AT[c][rp + row] = q3;
     } else if (lane < 45) {
       const int e = lane - 36, c = e / 3, row = e - c * 3;
-      AT[9 + c][rp + 6 + row] = p3;
+      AT[9 + c][rp + 6 + row] = q3;
     } else if (lane < 51) {
-      rT[rp + lane - 45] = p3;
+      rT[rp + lane - 45] = q3;
     } else if (lane < 54) {
-      rT[rp + 6 + lane - 51] = p3;
+      rT[rp + 6 + lane - 51] = q3;
     }
   }
   wave_order();
@@ -832,17 +848,38 @@ __global__ __launch_bounds__(256, OCC) void gn_twisted_kernel(GnArgs a) {
     // the next frame's loads are issued before the current frame is built, so the
     // factors' memory latency is off the chain
     const int n = wv == 0 ? m + 1 : nb;
-    GnFrameLoads<RP> nx;
-    if (n > 0) gn_load_frame<RP>(a, f0 + (wv == 0 ? 0 : L - 1), nx);
-    for (int j = 0; j < n; ++j) {
+    if (RP != 34 || !a.zero_each) gn_zero_stage<RP>(st[wv]);
+    // two load sets used alternately (frame j from set j & 1 while frame j + 1's loads go to
+    // the other): no register copy between them, so nothing waits for the next frame's
+    // loads before the current frame is built
+    GnFrameLoads<RP> ld0, ld1;
+    if (n > 0) gn_load_frame<RP>(a, f0 + (wv == 0 ? 0 : L - 1), ld0);
+    auto step = [&](int j, const GnFrameLoads<RP>& cu, GnFrameLoads<RP>& nx) __attribute__((always_inline)) {
       const int l = wv == 0 ? j : L - 1 - j;
-      const GnFrameLoads<RP> cu = nx;
       if (j + 1 < n) gn_load_frame<RP>(a, f0 + (wv == 0 ? l + 1 : l - 1), nx);
       while (lds_load_acquire(&consumed[wv]) < j - R + 2) __builtin_amdgcn_s_sleep(2);
       gn_stamp(a, t, 2 * l);
-      gn_build_frame<RP>(a, f0 + l, cu, st[wv], blk[wv][j % R]);
+      bool built = false;
+      if constexpr (RP == 34) {  // the A/B form (the general-K instantiation keeps one path: registers)
+        if (a.zero_each) {
+          gn_build_frame<RP, true>(a, f0 + l, cu, st[wv], blk[wv][j % R]);
+          built = true;
+        }
+      }
+      if (!built) gn_build_frame<RP, false>(a, f0 + l, cu, st[wv], blk[wv][j % R]);
       if (i == 0) lds_store_release(&ready[wv][j % R], j + 1);
       gn_stamp(a, t, 2 * l + 1);
+    };
+    if constexpr (RP == 34) {
+      for (int j = 0; j < n; j += 2) {
+        step(j, ld0, ld1);
+        if (j + 1 < n) step(j + 1, ld1, ld0);
+      }
+    } else {  // the general-K instantiation: one loop body (the unrolled pair spills there)
+      for (int j = 0; j < n; ++j) {
+        const GnFrameLoads<RP> cu = ld0;
+        step(j, cu, ld0);
+      }
     }
     return;
   }
@@ -958,7 +995,7 @@ static void launch_gn(const GnArgs& a, int v, hipStream_t s) {
     launch_gn_sv<RP, 0>(a, v & 7, s);
   else if (v & 16)
     launch_gn_sv<RP, 1>(a, v & 7, s);
-  else if (v & 32 || a.T > 2 * g_gn_cus())  // 32: force the 4-per-CU form
+  else if ((v & 32) || a.T > 2 * g_gn_cus())  // 32: force the 4-per-CU form
     hipLaunchKernelGGL((gn_twisted_kernel<RP, 4>), dim3(a.T), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((gn_twisted_kernel<RP, 2>), dim3(a.T), dim3(256), 0, s, a);
@@ -974,9 +1011,9 @@ int pa_debug_gn_set_trace(unsigned long long* trace_dev) {
 }
 
 int pa_debug_gn_set_assemblers(int na) {
-  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 64 && !((na & 8) && (na & 16)),
+  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 128 && !((na & 8) && (na & 16)),
            "gn variant %d: assembler waves (0..4) + 8 * legacy Cholesky or 16 * single-chain solver, 32: "
-           "two-ended kernel in its 4-per-CU form", na);
+           "two-ended kernel in its 4-per-CU form, 64: its staging re-zeroed every frame", na);
   pa::g_gn_na = na;
   return PA_OK;
 }
@@ -1002,7 +1039,7 @@ int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const do
            pa_trajectory_gn_workspace(T, L));
   const pa::GnArgs a{T,     L,      n_kp,   r_proj, j_proj, status_proj, r_dyn, j_dyn0, j_dyn1, j_dyn2, j_dyn3,
                      r_cv,  j_cv0,  j_cv1,  lambda, D,      E,           g,     delta,  info,   (double*)ws,
-                     pa::g_gn_trace};
+                     pa::g_gn_trace, (pa::g_gn_na & 64) ? 1 : 0};
   const hipStream_t s = (hipStream_t)stream;
   if (n_kp == 8)
     pa::launch_gn<34>(a, pa::g_gn_na, s);

@@ -610,6 +610,9 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
       if (g_trace) return run_stem4<16, 2, false, 4>(x, B, Cin, w, bias, out, s, RgbdSrc{}, g_trace);  // timestamps
       break;
     case 26: return run_stem4<16, 2, false, 5>(x, B, Cin, w, bias, out, s);  // timing only: idle movers
+    case 27: return run_stem4<8, 2>(x, B, Cin, w, bias, out, s);  // shorter bands at any batch (A/B)
+    case 28: return run_stem4<4, 2>(x, B, Cin, w, bias, out, s);
+    case 29: return run_stem4<32, 2>(x, B, Cin, w, bias, out, s);
     // shipped: version 4, the role split (29.3 vs 31.8 us per B = 64 launch, bit-identical;
     // prefetch depth 3 / 4 measured 29.7 / 30.4 us)
     default: break;
