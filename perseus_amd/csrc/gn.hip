@@ -38,7 +38,6 @@ struct GnArgs {
   int32_t* info;
   double* ws;
   unsigned long long* trace;  // timing only (pa_debug_gn_set_trace): 256 s_memrealtime stamps per trajectory
-  int zero_each;              // gn_twisted_kernel: re-zero the assembly staging every frame (A/B only)
 };
 
 // slot s of trajectory t's trace (lane 0 of the calling wave only)
@@ -69,13 +68,16 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 __device__ __forceinline__ void wave_order() { asm volatile("" ::: "memory"); }
 
 // RP factor rows padded to whole 4-row MFMA k-steps (the pad rows stay zero)
+// Rows 12..15 pad the variables to the MFMA's 16 so the operand reads need no lane test:
+// AT row 12 holds r (B's column 12 -> g), AT rows 13..15 are don't-care (they only feed
+// output rows / columns >= 13, never stored) and take the branch-free staging's dummy writes;
+// ANT / BT rows 12..15 stay zero.
 template <int RP>
 struct GnStage {
   static constexpr int RPP = (RP + 3) / 4 * 4;
-  double AT[gn::NV][RPP];
-  double rT[RPP];
-  double ANT[gn::NV][12];
-  double BT[gn::NV][12];
+  double AT[16][RPP];
+  double ANT[16][12];
+  double BT[16][12];
 };
 
 static __device__ int32_t gn_zero_i32[1];  // status source when no status array is given (zero-initialised)
@@ -171,10 +173,10 @@ __device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const Gn
   using namespace gn;
   constexpr int RPP = GnStage<RP>::RPP;
   constexpr int JR = GnFrameLoads<RP>::JR;
-  double(&AT)[NV][RPP] = st.AT;
-  double(&rT)[RPP] = st.rT;
-  double(&ANT)[NV][12] = st.ANT;
-  double(&BT)[NV][12] = st.BT;
+  double(&AT)[16][RPP] = st.AT;
+  double(&rT)[RPP] = st.AT[NV];
+  double(&ANT)[16][12] = st.ANT;
+  double(&BT)[16][12] = st.BT;
   const int lane = threadIdx.x & 63;
   const int t = (int)(f / a.L), l = (int)(f - (long)t * a.L);
   const int npair = a.L - 1;
@@ -197,79 +199,128 @@ __device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const Gn
     for (int e = lane; e < RPP; e += 64) rT[e] = 0.0;
     wave_order();
   }
-  // projections: rows 2k, 2k + 1; J column-major 2 x 6
-#pragma unroll
-  for (int q = 0; q < JR; ++q) {
-    const int e = lane + 64 * q;
-    if (e < K * 12) {
-      const int k = e / 12, c = (e - k * 12) >> 1, row = e & 1;
-      AT[c][2 * k + row] = js[q] == 0 ? jv[q] : 0.0;
-    }
-  }
-  if (vr) rT[lane] = rs == 0 ? rv : 0.0;
-  const int rn = 2 * K, rp = rn + 9;  // first row of the (l, l+1) / (l-1, l) blocks
-  if (nxt || !ZERO) {
-    const double m0 = nxt ? n0 : 0.0, m3 = nxt ? n3 : 0.0, m1 = nxt ? n1 : 0.0, m2 = nxt ? n2 : 0.0;
-    if (lane < 36) {  // dynamics: 6 x 6 / 6 x 3 / 6 x 3, column-major
-      const int c = lane / 6, row = lane - c * 6;
-      AT[c][rn + row] = m0;
-      ANT[c][row] = m0;
-      BT[c][row] = m3;
-      if (lane < 18) {
-        AT[6 + c][rn + row] = m1;
-        ANT[6 + c][row] = m1;
-        AT[9 + c][rn + row] = m2;
-        ANT[9 + c][row] = m2;
-      }
-    } else if (lane < 45) {  // const velocity: 3 x 3 on the velocity block
-      const int e = lane - 36, c = e / 3, row = e - c * 3;
-      AT[9 + c][rn + 6 + row] = m0;
-      ANT[9 + c][6 + row] = m0;
-      BT[9 + c][6 + row] = m3;
-    } else if (lane < 51) {
-      rT[rn + lane - 45] = m0;
-    } else if (lane < 54) {
-      rT[rn + 6 + lane - 51] = m0;
-    }
-  }
-  if (prv || !ZERO) {
-    const double q3 = prv ? p3 : 0.0;
-    if (lane < 36) {
-      const int c = lane / 6, row = lane - c * 6;
-      AT[c][rp + row] = q3;
-    } else if (lane < 45) {
-      const int e = lane - 36, c = e / 3, row = e - c * 3;
-      AT[9 + c][rp + 6 + row] = q3;
-    } else if (lane < 51) {
-      rT[rp + lane - 45] = q3;
-    } else if (lane < 54) {
-      rT[rp + 6 + lane - 51] = q3;
-    }
-  }
-  wave_order();
-  // [D_l | g_l] = A^T [A | r] and E_l = A_next^T B on the f64 matrix cores
-  // (v_mfma_f64_16x16x4_f64, MI355X_MICROARCH.md / cdna_hip_programming.md fragment maps:
-  // A operand lane l = (i = l & 15, k = l >> 4), B operand (k = l >> 4, j = l & 15),
-  // C/D lane l, register v = (row (l >> 4) + 4 v, col l & 15)).  Rows of the staged
-  // transposes are the k dimension, 4 per instruction; variables 12..15 are zero padding
-  // except B's column 12, which carries r so that C[:, 12] = A^T r = g.
   typedef double d4_t __attribute__((ext_vector_type(4)));
   const int li = lane & 15, lk = lane >> 4;
   d4_t cD = {0.0, 0.0, 0.0, 0.0}, cE = {0.0, 0.0, 0.0, 0.0};
+  const int rn = 2 * K, rp = rn + 9;  // first row of the (l, l+1) / (l-1, l) blocks
+  if constexpr (!ZERO) {
+    // branch-free staging: every lane writes its fixed positions (offsets in doubles from
+    // AT[0][0]; unused slots go to the don't-care row 13 + lane / RPP), selects instead of
+    // lane-class branches
+    double* S = &AT[0][0];
+    constexpr int OA = 0, ON = 16 * RPP, OB = 16 * RPP + 16 * 12;
+    const int dummy = 13 * RPP + lane;
 #pragma unroll
-  for (int q = 0; q < RPP / 4; ++q) {
-    const int row = 4 * q + lk;
-    const double at = li < NV ? AT[li][row] : 0.0;
-    const double bv = li < NV ? at : (li == NV ? rT[row] : 0.0);
-    cD = __builtin_amdgcn_mfma_f64_16x16x4f64(at, bv, cD, 0, 0, 0);
-  }
-  if (nxt) {
+    for (int q = 0; q < JR; ++q) {
+      const int e = lane + 64 * q;
+      const int k = e / 12, c = (e - k * 12) >> 1, row = e & 1;
+      S[e < K * 12 ? OA + c * RPP + 2 * k + row : dummy] = js[q] == 0 ? jv[q] : 0.0;
+    }
+    S[vr ? OA + NV * RPP + lane : dummy] = rs == 0 ? rv : 0.0;
+    const double m0 = nxt ? n0 : 0.0, m3 = nxt ? n3 : 0.0, m1 = nxt ? n1 : 0.0, m2 = nxt ? n2 : 0.0;
+    const double q3 = prv ? p3 : 0.0;
+    const bool d36 = lane < 36, c9 = lane >= 36 && lane < 45, r6 = lane >= 45 && lane < 51, r3 = lane >= 51 && lane < 54;
+    const int c6 = lane / 6, w6 = lane - c6 * 6;                  // dynamics: column, row
+    const int c3 = (lane - 36) / 3, w3 = (lane - 36) - c3 * 3;    // const velocity (lane 36..44)
+    auto at_row = [&](int r0) {  // AT offset of this lane's (l, l+1) or (l-1, l) element (rows from r0)
+      return d36 ? OA + c6 * RPP + r0 + w6
+           : c9  ? OA + (9 + c3) * RPP + r0 + 6 + w3
+           : r6  ? OA + NV * RPP + r0 + lane - 45
+           : r3  ? OA + NV * RPP + r0 + 6 + lane - 51
+                 : dummy;
+    };
+    S[at_row(rn)] = m0;
+    S[d36 ? ON + c6 * 12 + w6 : c9 ? ON + (9 + c3) * 12 + 6 + w3 : dummy] = m0;
+    S[d36 ? OB + c6 * 12 + w6 : c9 ? OB + (9 + c3) * 12 + 6 + w3 : dummy] = m3;
+    const bool d18 = lane < 18;
+    S[d18 ? OA + (6 + c6) * RPP + rn + w6 : dummy] = m1;
+    S[d18 ? ON + (6 + c6) * 12 + w6 : dummy] = m1;
+    S[d18 ? OA + (9 + c6) * RPP + rn + w6 : dummy] = m2;
+    S[d18 ? ON + (9 + c6) * 12 + w6 : dummy] = m2;
+    S[at_row(rp)] = q3;
+    wave_order();
+    // [D_l | g_l] = A^T [A | r], E_l = A_next^T B: the operands straight from the padded rows
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < RPP / 4; ++q) {
+      const double v = AT[li][4 * q + lk];
+      cD = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, cD, 0, 0, 0);
+    }
+    if (nxt) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        cE = __builtin_amdgcn_mfma_f64_16x16x4f64(ANT[li][4 * q + lk], BT[li][4 * q + lk], cE, 0, 0, 0);
+    }
+  } else {
+    // projections: rows 2k, 2k + 1; J column-major 2 x 6
+#pragma unroll
+    for (int q = 0; q < JR; ++q) {
+      const int e = lane + 64 * q;
+      if (e < K * 12) {
+        const int k = e / 12, c = (e - k * 12) >> 1, row = e & 1;
+        AT[c][2 * k + row] = js[q] == 0 ? jv[q] : 0.0;
+      }
+    }
+    if (vr) rT[lane] = rs == 0 ? rv : 0.0;
+    if (nxt || !ZERO) {
+      const double m0 = nxt ? n0 : 0.0, m3 = nxt ? n3 : 0.0, m1 = nxt ? n1 : 0.0, m2 = nxt ? n2 : 0.0;
+      if (lane < 36) {  // dynamics: 6 x 6 / 6 x 3 / 6 x 3, column-major
+        const int c = lane / 6, row = lane - c * 6;
+        AT[c][rn + row] = m0;
+        ANT[c][row] = m0;
+        BT[c][row] = m3;
+        if (lane < 18) {
+          AT[6 + c][rn + row] = m1;
+          ANT[6 + c][row] = m1;
+          AT[9 + c][rn + row] = m2;
+          ANT[9 + c][row] = m2;
+        }
+      } else if (lane < 45) {  // const velocity: 3 x 3 on the velocity block
+        const int e = lane - 36, c = e / 3, row = e - c * 3;
+        AT[9 + c][rn + 6 + row] = m0;
+        ANT[9 + c][6 + row] = m0;
+        BT[9 + c][6 + row] = m3;
+      } else if (lane < 51) {
+        rT[rn + lane - 45] = m0;
+      } else if (lane < 54) {
+        rT[rn + 6 + lane - 51] = m0;
+      }
+    }
+    if (prv || !ZERO) {
+      const double q3 = prv ? p3 : 0.0;
+      if (lane < 36) {
+        const int c = lane / 6, row = lane - c * 6;
+        AT[c][rp + row] = q3;
+      } else if (lane < 45) {
+        const int e = lane - 36, c = e / 3, row = e - c * 3;
+        AT[9 + c][rp + 6 + row] = q3;
+      } else if (lane < 51) {
+        rT[rp + lane - 45] = q3;
+      } else if (lane < 54) {
+        rT[rp + 6 + lane - 51] = q3;
+      }
+    }
+    wave_order();
+    // [D_l | g_l] = A^T [A | r] and E_l = A_next^T B on the f64 matrix cores
+    // (v_mfma_f64_16x16x4_f64, MI355X_MICROARCH.md / cdna_hip_programming.md fragment maps:
+    // A operand lane l = (i = l & 15, k = l >> 4), B operand (k = l >> 4, j = l & 15),
+    // C/D lane l, register v = (row (l >> 4) + 4 v, col l & 15)).  Rows of the staged
+    // transposes are the k dimension, 4 per instruction; variables 12..15 are zero padding
+    // except B's column 12, which carries r so that C[:, 12] = A^T r = g.
+#pragma unroll
+    for (int q = 0; q < RPP / 4; ++q) {
       const int row = 4 * q + lk;
-      const double an = li < NV ? ANT[li][row] : 0.0;
-      const double bt = li < NV ? BT[li][row] : 0.0;
-      cE = __builtin_amdgcn_mfma_f64_16x16x4f64(an, bt, cE, 0, 0, 0);
+      const double at = li < NV ? AT[li][row] : 0.0;
+      const double bv = li < NV ? at : (li == NV ? rT[row] : 0.0);
+      cD = __builtin_amdgcn_mfma_f64_16x16x4f64(at, bv, cD, 0, 0, 0);
+    }
+    if (nxt) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int row = 4 * q + lk;
+        const double an = li < NV ? ANT[li][row] : 0.0;
+        const double bt = li < NV ? BT[li][row] : 0.0;
+        cE = __builtin_amdgcn_mfma_f64_16x16x4f64(an, bt, cE, 0, 0, 0);
+      }
     }
   }
   double* Dl = a.D + f * NB;
@@ -848,38 +899,23 @@ __global__ __launch_bounds__(256, OCC) void gn_twisted_kernel(GnArgs a) {
     // the next frame's loads are issued before the current frame is built, so the
     // factors' memory latency is off the chain
     const int n = wv == 0 ? m + 1 : nb;
-    if (RP != 34 || !a.zero_each) gn_zero_stage<RP>(st[wv]);
-    // two load sets used alternately (frame j from set j & 1 while frame j + 1's loads go to
-    // the other): no register copy between them, so nothing waits for the next frame's
-    // loads before the current frame is built
-    GnFrameLoads<RP> ld0, ld1;
+    gn_zero_stage<RP>(st[wv]);
+    // frame j + 1's loads are issued before frame j is built (an unrolled pair of load sets
+    // without the copy measured the same, 83.1 vs 84.4 us, and needs more registers)
+    GnFrameLoads<RP> ld0;
     if (n > 0) gn_load_frame<RP>(a, f0 + (wv == 0 ? 0 : L - 1), ld0);
     auto step = [&](int j, const GnFrameLoads<RP>& cu, GnFrameLoads<RP>& nx) __attribute__((always_inline)) {
       const int l = wv == 0 ? j : L - 1 - j;
       if (j + 1 < n) gn_load_frame<RP>(a, f0 + (wv == 0 ? l + 1 : l - 1), nx);
       while (lds_load_acquire(&consumed[wv]) < j - R + 2) __builtin_amdgcn_s_sleep(2);
       gn_stamp(a, t, 2 * l);
-      bool built = false;
-      if constexpr (RP == 34) {  // the A/B form (the general-K instantiation keeps one path: registers)
-        if (a.zero_each) {
-          gn_build_frame<RP, true>(a, f0 + l, cu, st[wv], blk[wv][j % R]);
-          built = true;
-        }
-      }
-      if (!built) gn_build_frame<RP, false>(a, f0 + l, cu, st[wv], blk[wv][j % R]);
+      gn_build_frame<RP, false>(a, f0 + l, cu, st[wv], blk[wv][j % R]);
       if (i == 0) lds_store_release(&ready[wv][j % R], j + 1);
       gn_stamp(a, t, 2 * l + 1);
     };
-    if constexpr (RP == 34) {
-      for (int j = 0; j < n; j += 2) {
-        step(j, ld0, ld1);
-        if (j + 1 < n) step(j + 1, ld1, ld0);
-      }
-    } else {  // the general-K instantiation: one loop body (the unrolled pair spills there)
-      for (int j = 0; j < n; ++j) {
-        const GnFrameLoads<RP> cu = ld0;
-        step(j, cu, ld0);
-      }
+    for (int j = 0; j < n; ++j) {
+      const GnFrameLoads<RP> cu = ld0;
+      step(j, cu, ld0);
     }
     return;
   }
@@ -1011,9 +1047,9 @@ int pa_debug_gn_set_trace(unsigned long long* trace_dev) {
 }
 
 int pa_debug_gn_set_assemblers(int na) {
-  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 128 && !((na & 8) && (na & 16)),
+  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 64 && !((na & 8) && (na & 16)),
            "gn variant %d: assembler waves (0..4) + 8 * legacy Cholesky or 16 * single-chain solver, 32: "
-           "two-ended kernel in its 4-per-CU form, 64: its staging re-zeroed every frame", na);
+           "two-ended kernel in its 4-per-CU form", na);
   pa::g_gn_na = na;
   return PA_OK;
 }
@@ -1039,7 +1075,7 @@ int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const do
            pa_trajectory_gn_workspace(T, L));
   const pa::GnArgs a{T,     L,      n_kp,   r_proj, j_proj, status_proj, r_dyn, j_dyn0, j_dyn1, j_dyn2, j_dyn3,
                      r_cv,  j_cv0,  j_cv1,  lambda, D,      E,           g,     delta,  info,   (double*)ws,
-                     pa::g_gn_trace, (pa::g_gn_na & 64) ? 1 : 0};
+                     pa::g_gn_trace};
   const hipStream_t s = (hipStream_t)stream;
   if (n_kp == 8)
     pa::launch_gn<34>(a, pa::g_gn_na, s);
