@@ -412,11 +412,59 @@ typedef double gn_d2 __attribute__((ext_vector_type(2)));
 // M E' (the S update reads it across lanes), z, this frame's b, the sweep's pivot rows.
 struct GnChainLds {
   double M[gn::NB];
-  double G[gn::NB];
+  double G[gn::NV * 13];  // gn_couple: G (row-major 12 x 12); gn_couple_mfma: E'^T [G | zprev] (12 x 13)
   double z[gn::NV];
   double bs[gn::NV];
   double rk2[2 * gn::NV];
 };
+
+// gn_couple on the f64 matrix cores (v_mfma_f64_16x16x4f64, operand maps as in
+// gn_build_frame): G = Mprev E' as 3 k-steps with A = Mprev (lane: row l & 15, k = l >> 4) and
+// B = E' (k = l >> 4, column l & 15); G lands in the C layout (register v: row (l >> 4) + 4v,
+// column l & 15), which for k-step q is exactly the B operand E'^T G needs (row 4q + (l >> 4)),
+// and E'^T's A operand is E' read as B was -- so the second product needs no exchange.
+// Column 12 of that B carries zprev, so T = E'^T [G | zprev] gives the b update too. T goes
+// through LDS (xch, 12 x 13) once to reach the row layout (lane: row r, columns c0 .. c0 + 3).
+// Gout (LDS, row-major) and gws (workspace) receive G when given.
+template <bool MIR>
+__device__ __forceinline__ void gn_couple_mfma(const double* Mprev, const double* zprev, const double* eb,
+                                               double* Gout, double* gws, double* xch, int r, int c0,
+                                               double (&sv)[4], double& b) {
+  using namespace gn;
+  typedef double d4_t __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const bool in = li < NV;
+  const int lr = in ? li : 0;  // a valid row / column for the lanes of the padding
+  double e[3];
+  d4_t cG = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int k = 4 * q + lk;
+    const double m = in ? Mprev[lr * NV + k] : 0.0;
+    e[q] = in ? (MIR ? eb[lr * NV + k] : eb[k * NV + lr]) : 0.0;  // E'(k, li)
+    cG = __builtin_amdgcn_mfma_f64_16x16x4f64(m, e[q], cG, 0, 0, 0);
+  }
+  d4_t cT = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const double bz = li == NV ? zprev[4 * q + lk] : 0.0;
+    cT = __builtin_amdgcn_mfma_f64_16x16x4f64(e[q], in ? cG[q] : bz, cT, 0, 0, 0);
+  }
+  wave_order();  // every lane is past its reads of xch / Gout's previous contents
+#pragma unroll
+  for (int v = 0; v < 3; ++v) {  // rows lk + 4v < 12
+    const int i = lk + 4 * v;
+    if (li <= NV) xch[i * 13 + li] = cT[v];
+    if (in) {
+      if (Gout) Gout[i * NV + li] = cG[v];
+      if (gws) gws[i * NV + li] = cG[v];
+    }
+  }
+  wave_order();
+#pragma unroll
+  for (int c = 0; c < 4; ++c) sv[c] -= xch[r * 13 + c0 + c];  // (8-byte aligned rows)
+  b -= xch[r * 13 + NV];
+}
 
 // (sv, b) -= the coupling to the previously eliminated frame (lane: row r, columns c0 .. c0 + 3):
 //   G = Mprev E',   sv -= E'^T G,   b -= E'^T zprev,
@@ -951,11 +999,11 @@ __global__ __launch_bounds__(256, OCC) void gn_twisted_kernel(GnArgs a) {
       double b = -bc[2 * NB + r];
       if (j > 0) {
         if (sc == 0)  // G_{l-1} = M_{l-1} E_{l-1} -> workspace slot l - 1
-          gn_couple<false, CU>(C.M, C.z, blk[0][prv] + NB, C.G, ws + (size_t)(l - 1) * GN_WSF, r, c0, act, sv, b);
+          gn_couple_mfma<false>(C.M, C.z, blk[0][prv] + NB, nullptr, ws + (size_t)(l - 1) * GN_WSF, C.G, r, c0, sv, b);
         else  // H_{l+1} = N_{l+1} E_l^T -> workspace slot l + 1
-          gn_couple<true, CU>(C.M, C.z, bc + NB, C.G, ws + (size_t)(l + 1) * GN_WSF, r, c0, act, sv, b);
+          gn_couple_mfma<true>(C.M, C.z, bc + NB, nullptr, ws + (size_t)(l + 1) * GN_WSF, C.G, r, c0, sv, b);
       }
-      if (merge) gn_couple<true, CU>(ch[1].M, ch[1].z, bc + NB, Hm, nullptr, r, c0, act, sv, b);
+      if (merge) gn_couple_mfma<true>(ch[1].M, ch[1].z, bc + NB, Hm, nullptr, C.G, r, c0, sv, b);
       gn_stamp(a, t, 66 + 4 * l);
       if (!gn_sweep(sv, C.rk2, r, c0, act)) {
         info = l + 1;  // idles through the remaining frames' hand-overs
