@@ -95,7 +95,8 @@ int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s);
 int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s);
 // the same convs split-K + a fixed-order reduce (small batches, conv_splitk.hip): a.part
 // holds splitk_part_floats(B) floats
-int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s);
+// (layer2 runs unsplit on small tiles unless split_l2, the A/B form)
+int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s, bool split_l2 = false);
 // stride-2 block entries for small batches: layer2 on one-tile workgroups, layer4 split-K with
 // the conv and the downsample reduced in one pass (layer3's batched kernel is kept)
 int launch_conv3x3s2_small(const ConvS2Args& a, hipStream_t s, const char** kname);

@@ -76,15 +76,19 @@ size_t splitk_part_floats(int B) {
   return (size_t)B * 262144;
 }
 
-int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s) {
+int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s, bool split_l2) {
   PA_CHECK(a.stride == 1 && a.pad == 1 && (a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES)),
            "split-K conv: stride-1, relu (+residual) only (epi %d)", a.epi);
   PA_CHECK(a.B <= 64, "split-K conv: batch %d above 64", a.B);
   if (a.B <= 0) return PA_OK;
   int rc;
-  if (a.Cin == 128 && a.Cout == 128 && a.Hout == 32 && a.Wout == 32)
+  if (a.Cin == 128 && a.Cout == 128 && a.Hout == 32 && a.Wout == 32) {
+    // layer2: no split -- the batched kernel's 8 x 16 tile form (gx variant 1, 4 waves, 18 steps:
+    // 48 workgroups at B = 3), 9.7 us per forward faster than 2 splits + reduce
+    // (profiles/r03aa/ab_l2.log) and bit-identical to the batched path
+    if (!split_l2) return launch_conv3x3_gx_l2(a, 1, s);
     rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 2>(a, s);
-  else if (a.Cin == 256 && a.Cout == 256 && a.Hout == 16 && a.Wout == 16)
+  } else if (a.Cin == 256 && a.Cout == 256 && a.Hout == 16 && a.Wout == 16)
     rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 4>(a, s);
   else if (a.Cin == 512 && a.Cout == 512 && a.Hout == 8 && a.Wout == 8)
     rc = run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8>(a, s);

@@ -339,11 +339,13 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   auto conv_s1 = [&](ConvArgs& a, const char** kn) -> int {
     if constexpr (std::is_same<T, _Float16>::value) {
       const int layer = a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : a.Hout == 8 ? 4 : 0;
-      if (layer && B <= d->splitk_max && g_variant[layer] == 0 && !(a.epi & EPI_HEAD)) {
-        static const char* names[5] = {"", "", "conv3x3x_l2_splitk", "conv3x3x_l3_splitk", "conv3x3x_l4_splitk"};
-        *kn = names[layer];
+      // g_variant[layer] == 71: layer2 split as well (A/B)
+      if (layer && B <= d->splitk_max && (g_variant[layer] == 0 || g_variant[layer] == 71) && !(a.epi & EPI_HEAD)) {
+        const bool split_l2 = g_variant[layer] == 71;
+        static const char* names[5] = {"", "", "conv3x3x_l2_small", "conv3x3x_l3_splitk", "conv3x3x_l4_splitk"};
+        *kn = (layer == 2 && split_l2) ? "conv3x3x_l2_splitk" : names[layer];
         a.part = d->part;
-        return launch_conv3x3_splitk(a, s);
+        return launch_conv3x3_splitk(a, s, split_l2);
       }
     }
     return launch_conv3x3_s1<T>(a, s, kn);

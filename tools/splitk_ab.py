@@ -19,7 +19,9 @@ def main():
     p.add_argument("--batches", default="1,3,8")
     p.add_argument("--reps", type=int, default=200)
     p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--variants", default="", help="a third mode: split-K plus these kernel variants, e.g. 2:51,6:12")
     a = p.parse_args()
+    extra = {int(k): int(v) for k, v in (kv.split(":") for kv in a.variants.split(",") if kv)}
     import numpy as np
     import torch
 
@@ -31,10 +33,12 @@ def main():
     for B in [int(b) for b in a.batches.split(",")]:
         x = torch.from_numpy(synth.synthetic_frames(0, B)).to(dev)
         graphs = {}
-        for mode, sk in (("batched", 0), ("split_k", B)):
+        modes = [("batched", 0, {}), ("split_k", B, {})] + ([("split_k+variants", B, extra)] if extra else [])
+        for mode, sk, var in modes:
             m = KeypointCNN(num_channels=4)
             m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
             m.set_split_k(sk)
+            m.set_variants(var)
             y = torch.empty((B, 16), dtype=torch.float32, device=dev)
             s = torch.cuda.Stream(dev)
             with torch.cuda.stream(s):
