@@ -228,6 +228,10 @@ int pa_window_advance(int T, int L, int n_kp, const float* y_new_dev, float* y_d
                       double* angvel_dev, double* vel_dev, double dt, int vel_frame, void* stream);
 int pa_window_retract(int T, int L, const double* delta_dev, const int32_t* info_dev, double* pose_dev,
                       double* angvel_dev, double* vel_dev, void* stream);
+/* pa_window_retract that also writes each trajectory's newest (last-frame) pose after the
+ * update to newest_pose_dev (T, 12) -- the streaming tick's pose output, no strided gather. */
+int pa_window_retract_newest(int T, int L, const double* delta_dev, const int32_t* info_dev, double* pose_dev,
+                             double* angvel_dev, double* vel_dev, double* newest_pose_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -69,6 +69,7 @@ _SIGS = {
                                                                                      C.c_void_p]),
     "pa_window_retract": (C.c_int, [C.c_int, C.c_int] + [C.c_void_p] * 6),
     "pa_debug_gn_set_assemblers": (C.c_int, [C.c_int]),
+    "pa_window_retract_newest": (C.c_int, [C.c_int, C.c_int] + [C.c_void_p] * 7),
     "pa_debug_gn_set_trace": (C.c_int, [C.c_void_p]),
     "pa_loss_statistics_workspace": (C.c_size_t, [C.c_longlong]),
     "pa_loss_statistics": (C.c_int, [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),

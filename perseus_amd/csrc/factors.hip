@@ -968,21 +968,36 @@ __global__ __launch_bounds__(256) void window_advance_kernel(int L, int n_kp, co
 // with the Expmap chart, tangent [omega; v]), angvel += delta[6:9], vel += delta[9:12]
 // (pa_trajectory_gn_step's variable block); trajectories whose step failed (info != 0)
 // keep their values.
+// newest (optional): each trajectory's last-frame pose after the update (T, 12), the
+// streaming tick's output, so it needs no gather of the strided window
 __global__ __launch_bounds__(64) void window_retract_kernel(int T, int L, const double* __restrict__ delta,
                                                             const int32_t* __restrict__ info, double* pose,
-                                                            double* angvel, double* vel) {
+                                                            double* angvel, double* vel, double* newest) {
   const long f = (long)blockIdx.x * 64 + threadIdx.x;
   if (f >= (long)T * L) return;
-  if (info && info[f / L] != 0) return;
+  const long t = f / L;
+  double* o = pose + f * 12;
+  double* no = (newest && f - t * L == L - 1) ? newest + t * 12 : nullptr;
+  if (info && info[t] != 0) {  // unsolved: the window stays
+    if (no)
+#pragma unroll
+      for (int i = 0; i < 12; ++i) no[i] = o[i];
+    return;
+  }
   const double* d = delta + f * 12;
   const V3 dw = load3(d), dv = load3(d + 3);
-  const Pose P = compose(load_pose(pose + f * 12), pose_exp(dw, dv, ang(dw)));
-  double* o = pose + f * 12;
+  const Pose P = compose(load_pose(o), pose_exp(dw, dv, ang(dw)));
+  double v[12];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) o[i] = P.R.a[i];
-  o[9] = P.t.x;
-  o[10] = P.t.y;
-  o[11] = P.t.z;
+  for (int i = 0; i < 9; ++i) v[i] = P.R.a[i];
+  v[9] = P.t.x;
+  v[10] = P.t.y;
+  v[11] = P.t.z;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) o[i] = v[i];
+  if (no)
+#pragma unroll
+    for (int i = 0; i < 12; ++i) no[i] = v[i];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     angvel[f * 3 + i] += d[6 + i];
@@ -1006,16 +1021,21 @@ int pa_window_advance(int T, int L, int n_kp, const float* y_new, float* y, doub
   return PA_OK;
 }
 
-int pa_window_retract(int T, int L, const double* delta, const int32_t* info, double* pose, double* angvel,
-                      double* vel, void* stream) {
+int pa_window_retract_newest(int T, int L, const double* delta, const int32_t* info, double* pose, double* angvel,
+                             double* vel, double* newest_pose, void* stream) {
   PA_CHECK(T >= 0 && L >= 1, "T=%d L=%d", T, L);
   if (T == 0) return PA_OK;
   PA_CHECK(delta && pose && angvel && vel, "null pointer");
   const long n = (long)T * L;
   hipLaunchKernelGGL(pa::window_retract_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
-                     T, L, delta, info, pose, angvel, vel);
+                     T, L, delta, info, pose, angvel, vel, newest_pose);
   PA_LAUNCH_CHECK();
   return PA_OK;
+}
+
+int pa_window_retract(int T, int L, const double* delta, const int32_t* info, double* pose, double* angvel,
+                      double* vel, void* stream) {
+  return pa_window_retract_newest(T, L, delta, info, pose, angvel, vel, nullptr, stream);
 }
 
 int pa_dyn_linearize(int n, const double* t1, const double* w, const double* v, const double* t2, double dt,

@@ -197,12 +197,19 @@ def window_advance(y_new: torch.Tensor, win: dict, *, dt: float, vel_frame: str 
             _lib.stream_of(dev)), "pa_window_advance")
 
 
-def window_retract(win: dict, delta: torch.Tensor, info: torch.Tensor | None = None) -> None:
+def window_retract(win: dict, delta: torch.Tensor, info: torch.Tensor | None = None,
+                   newest: torch.Tensor | None = None) -> None:
     """pa_window_retract on the device's current stream: pose <- pose Exp(delta[:6]),
-    angvel += delta[6:9], vel += delta[9:12]; trajectories with info != 0 unchanged."""
+    angvel += delta[6:9], vel += delta[9:12]; trajectories with info != 0 unchanged.
+    newest (optional, contiguous f64 (T, 12) on the device): each trajectory's last-frame
+    pose after the update (pa_window_retract_newest)."""
     T, L = win["pose"].shape[:2]
     dev = win["pose"].device
+    if newest is not None and (newest.device != dev or newest.dtype != torch.float64 or newest.numel() != T * 12
+                               or not newest.is_contiguous()):
+        raise RuntimeError(f"newest must be a contiguous float64 ({T}, 12) tensor on {dev}")
     with torch.cuda.device(dev):
-        _lib.check(_lib.lib().pa_window_retract(T, L, delta.data_ptr(), _lib.ptr(info), win["pose"].data_ptr(),
-                                                win["angvel"].data_ptr(), win["vel"].data_ptr(), _lib.stream_of(dev)),
+        _lib.check(_lib.lib().pa_window_retract_newest(T, L, delta.data_ptr(), _lib.ptr(info), win["pose"].data_ptr(),
+                                                       win["angvel"].data_ptr(), win["vel"].data_ptr(),
+                                                       _lib.ptr(newest), _lib.stream_of(dev)),
                    "pa_window_retract")

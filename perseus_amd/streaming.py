@@ -14,12 +14,12 @@ Gauss-Newton step per tick.  Per tick:
   host: frames -> pinned staging (centre crop rows only, or the full frame)
   GPU (one hipGraph replay on a private stream): H2D -> pa_detector_forward_rgbd_px
        (B = n_cams; the preprocess runs inside the stem's row loads, the denormalize in the
-       head; fp32: pa_preprocess_rgbd + pa_detector_forward + pa_keypoints_postprocess) -> D2H
-       pixels
+       head; fp32: pa_preprocess_rgbd + pa_detector_forward + pa_keypoints_postprocess)
        [pose stage] -> pa_window_advance (window shifts one frame, the new keypoints
        appended, the new pose predicted by the dynamics model) -> pa_trajectory_linearize
        (whitened factors of every camera's window) -> pa_trajectory_gn_step ->
-       pa_window_retract (pose Exp(delta), velocities += delta) -> D2H newest poses + info
+       pa_window_retract_newest (pose Exp(delta), velocities += delta, newest poses out)
+       -> ONE D2H of [pixels | info | newest poses] (and one H2D of [rgb | depth] at the start)
   host: wait for the replay, return (n_cams, K, 2) pixel coordinates (and the poses).
 
 The graph removes the per-launch CPU cost of the ~26 launches (the forward at B=3
@@ -66,14 +66,31 @@ class StreamingPipeline:
         self.sh, self.sw = sh, sw
         self.r0, self.c0 = self.Hs // 2 - self.H // 2, self.Ws // 2 - self.W // 2
         n, K = n_cams, model.n_keypoints
-        self.rgb_h = torch.empty((n, sh, sw, 3), dtype=torch.uint8).pin_memory()
-        self.depth_h = torch.empty((n, sh, sw), dtype=torch.float32).pin_memory()
-        self.px_h = torch.empty((n, K, 2), dtype=torch.float32).pin_memory()
-        self.rgb_d = torch.empty((n, sh, sw, 3), dtype=torch.uint8, device=self.dev)
-        self.depth_d = torch.empty((n, sh, sw), dtype=torch.float32, device=self.dev)
+        # One staging block per direction, so a tick is one H2D and one D2H copy (each copy is a
+        # ~5-12 us operation on the stream, and a copy enqueued between kernels stalls them):
+        #   in  = [rgb (n, sh, sw, 3) u8 | depth (n, sh, sw) f32]
+        #   out = [px (n, K, 2) f32 | info (n,) i32 | pad to 8 B | newest pose (n, 12) f64]
+        nr = n * sh * sw * 3
+        if nr % 4:
+            raise ValueError(f"staging: {n} x {sh} x {sw} RGB bytes not 4-aligned for the depth block")
+        nin = nr + n * sh * sw * 4
+        self._po = ((n * K * 2 + n) * 4 + 7) // 8 * 8
+        nout = self._po + n * 12 * 8
+        self.in_h = torch.empty(nin, dtype=torch.uint8).pin_memory()
+        self.in_d = torch.empty(nin, dtype=torch.uint8, device=self.dev)
+        self.out_h = torch.zeros(nout, dtype=torch.uint8).pin_memory()
+        self.out_d = torch.zeros(nout, dtype=torch.uint8, device=self.dev)
+
+        def views(i, o):
+            return (i[:nr].view(n, sh, sw, 3), i[nr:].view(torch.float32).view(n, sh, sw),
+                    o[:n * K * 8].view(torch.float32).view(n, K, 2),
+                    o[n * K * 8:n * K * 8 + n * 4].view(torch.int32),
+                    o[self._po:].view(torch.float64).view(n, 12))
+
+        self.rgb_h, self.depth_h, self.px_h, self.info_h, self.pose_h = views(self.in_h, self.out_h)
+        self.rgb_d, self.depth_d, self.px_d, self.info_d, self.pose_d = views(self.in_d, self.out_d)
         self.x = torch.empty((n, 4, self.H, self.W), dtype=torch.float32, device=self.dev)
         self.y = torch.empty((n, 2 * K), dtype=torch.float32, device=self.dev)
-        self.px_d = torch.empty((n, K, 2), dtype=torch.float32, device=self.dev)
         self.stream = torch.cuda.Stream(self.dev)
         # A private handle: the captured graph holds its weight and workspace pointers, so
         # nothing the model does later (a larger batch growing its workspace, a weight
@@ -106,11 +123,10 @@ class StreamingPipeline:
             self.graph = g
 
     def _enqueue(self):
-        """H2D, preprocess, forward, postprocess, D2H on the current stream."""
+        """H2D, preprocess, forward, postprocess, [pose stage], D2H on the current stream."""
         L = _lib.lib()
         s = torch.cuda.current_stream(self.dev).cuda_stream
-        self.rgb_d.copy_(self.rgb_h, non_blocking=True)
-        self.depth_d.copy_(self.depth_h, non_blocking=True)
+        self.in_d.copy_(self.in_h, non_blocking=True)
         if self.model.precision != "fp16":  # fp32 / fp16x3: preprocess kernel, then the forward
             _lib.check(L.pa_preprocess_rgbd(self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n, self.sh, self.sw,
                                             int(self.bgr), self.near, self.far, self.H, self.W, self.x.data_ptr(), s),
@@ -122,15 +138,12 @@ class StreamingPipeline:
             _lib.check(L.pa_detector_forward_rgbd_px(self._h, self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n,
                                                      self.sh, self.sw, int(self.bgr), self.near, self.far,
                                                      self.y.data_ptr(), self.px_d.data_ptr(), s), "forward_rgbd_px")
-        self.px_h.copy_(self.px_d, non_blocking=True)
         if self.pose_L:  # the pose stage, all on this stream (HBM-resident window)
             pipeline.window_advance(self.y, self.win, dt=self.dt, vel_frame=self.vel_frame)
             pipeline.launch(self.traj_args, self.dev)
-            self.gn.launch()
-            pipeline.window_retract(self.win, self.gn.out["delta"], self.gn.out["info"])
-            self.pose_d.copy_(self.win["pose"][:, -1])
-            self.pose_h.copy_(self.pose_d, non_blocking=True)
-            self.info_h.copy_(self.gn.out["info"], non_blocking=True)
+            self.gn.launch()  # info straight into the output block
+            pipeline.window_retract(self.win, self.gn.out["delta"], self.gn.out["info"], newest=self.pose_d)
+        self.out_h.copy_(self.out_d, non_blocking=True)  # pixels (+ info, newest poses): one D2H
 
     def _init_pose_stage(self, K, corners, dt, vel_frame, proj_sigma, dyn_sigma, cv_sigma, lam, init_pose, init_vel,
                          init_angvel):
@@ -159,9 +172,7 @@ class StreamingPipeline:
         for k in ("y", "pose", "vel", "angvel"):  # linearize reads the window in place, no staging copy
             assert self.lin["_keep"][("y", "pose", "vel", "angvel").index(k)].data_ptr() == self.win[k].data_ptr()
         self.gn = pipeline.GNPlan(self.lin, T=n, L=Lw, lam=lam)
-        self.pose_d = torch.empty((n, 12), **f64)
-        self.pose_h = torch.empty((n, 12), dtype=torch.float64).pin_memory()
-        self.info_h = torch.empty((n,), dtype=torch.int32).pin_memory()
+        self.gn.out["info"] = self.info_d  # the GN step writes info into the output block
 
     def reset_window(self) -> None:
         """Every frame of every camera's window back to the initial state (keypoints 0)."""
