@@ -82,6 +82,13 @@ int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s, bool split_l2) {
   PA_CHECK(a.B <= 64, "split-K conv: batch %d above 64", a.B);
   if (a.B <= 0) return PA_OK;
   int rc;
+  if (a.Cin == 64 && a.Cout == 64 && a.Hout == 64 && a.Wout == 64) {
+    // layer1: the gx kernel on 8 x 16 tiles (4 waves, 9 steps, weights streamed per tap: 96
+    // workgroups at B = 3) instead of the weight-resident persistent kernel, whose every
+    // workgroup first stages all 73 KB of weights
+    if (!split_l2) return run_gx<8, 16, 1, 64, 2, 2, 64, 3>(a, false, s);
+    return launch_conv3x3_c64d(a, 0, s);
+  }
   if (a.Cin == 128 && a.Cout == 128 && a.Hout == 32 && a.Wout == 32) {
     // layer2: no split -- the batched kernel's 8 x 16 tile form (gx variant 1, 4 waves, 18 steps:
     // 48 workgroups at B = 3), 9.7 us per forward faster than 2 splits + reduce

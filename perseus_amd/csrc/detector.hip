@@ -338,12 +338,13 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   // stride-1 convs: split-K form for small batches (pa_detector_set_split_k, conv_splitk.hip)
   auto conv_s1 = [&](ConvArgs& a, const char** kn) -> int {
     if constexpr (std::is_same<T, _Float16>::value) {
-      const int layer = a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : a.Hout == 8 ? 4 : 0;
-      // g_variant[layer] == 71: layer2 split as well (A/B)
+      const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : a.Hout == 8 ? 4 : 0;
+      // g_variant[layer] == 71 (A/B): layer2 split as well, layer1 on the persistent kernel
       if (layer && B <= d->splitk_max && (g_variant[layer] == 0 || g_variant[layer] == 71) && !(a.epi & EPI_HEAD)) {
         const bool split_l2 = g_variant[layer] == 71;
-        static const char* names[5] = {"", "", "conv3x3x_l2_small", "conv3x3x_l3_splitk", "conv3x3x_l4_splitk"};
-        *kn = (layer == 2 && split_l2) ? "conv3x3x_l2_splitk" : names[layer];
+        static const char* names[5] = {"", "conv3x3x_l1_small", "conv3x3x_l2_small", "conv3x3x_l3_splitk",
+                                       "conv3x3x_l4_splitk"};
+        *kn = (layer == 2 && split_l2) ? "conv3x3x_l2_splitk" : (layer == 1 && split_l2) ? "conv3x3c64_l1" : names[layer];
         a.part = d->part;
         return launch_conv3x3_splitk(a, s, split_l2);
       }

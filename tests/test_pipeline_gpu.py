@@ -155,3 +155,24 @@ def test_full_size_config3_sampled_vs_oracle():
     assert int(out["status"].sum()) == 0 and torch.isfinite(out["j_proj"]).all()
     v = torch.as_tensor(tr["vels"], device="cuda").reshape(T, L, 3)
     assert torch.equal(out["r_cv"].reshape(T, L - 1, 3), v[:, 1:] - v[:, :-1])
+
+
+def test_window_retract_newest_vs_oracle():
+    """pa_window_retract_newest (the streaming tick's pose output): the window retract of
+    oracle/factors_ref.window_retract, plus each trajectory's newest pose after it -- also
+    for a trajectory the GN step did not solve (info != 0: window and newest pose unchanged)."""
+    T, L = 3, 5
+    poses, vels, angvels, _ = _problem(T, L, 9)
+    rng = np.random.default_rng(3)
+    delta = 0.05 * rng.standard_normal((T * L, 12))
+    info = np.array([0, 2, 0], dtype=np.int32)
+    win = {"pose": poses.reshape(T, L, 12), "vel": vels.reshape(T, L, 3), "angvel": angvels.reshape(T, L, 3)}
+    dwin = {k: torch.as_tensor(np.ascontiguousarray(v), device="cuda") for k, v in win.items()}
+    newest = torch.full((T, 12), float("nan"), dtype=torch.float64, device="cuda")
+    pipeline.window_retract(dwin, torch.as_tensor(delta, device="cuda"), torch.as_tensor(info, device="cuda"),
+                            newest=newest)
+    ref = F.window_retract(win, delta, info)
+    for k in ("pose", "vel", "angvel"):
+        np.testing.assert_allclose(dwin[k].cpu().numpy(), ref[k], rtol=0, atol=1e-12, err_msg=k)
+    np.testing.assert_array_equal(newest.cpu().numpy(), dwin["pose"][:, -1].cpu().numpy())
+    np.testing.assert_array_equal(newest.cpu().numpy()[1], poses.reshape(T, L, 12)[1, -1])
