@@ -78,3 +78,26 @@ def test_graph_survives_model_reallocation_and_reload():
     m(torch.from_numpy(synth.synthetic_frames(0, 2)).cuda())  # new weights: the model's handle is recreated
     np.testing.assert_array_equal(g(rgb, d), ref)  # the pipeline keeps the weights it was built with
     g.close()
+
+
+@pytest.mark.parametrize("n", [1, 5])
+def test_camera_counts_latency_mode_vs_batched_and_oracle(model, n):
+    """Other camera counts through the latency mode: the pipeline's pixels are the bits of
+    model.set_split_k(n) + forward on the same frames, within 0.05 px of the batched
+    kernels', and within the fp16 budget of the f64 oracle (streaming.py:68-80 arithmetic)."""
+    rgb, d = _frames(11, n)
+    pipe = StreamingPipeline(model, n_cams=n)
+    out = pipe(rgb, d)
+    pipe.close()
+    x = preprocess_rgbd(torch.as_tensor(rgb).cuda(), torch.as_tensor(d).cuda())
+    model.set_split_k(n)
+    try:
+        y = model(x)
+    finally:
+        model.set_split_k(0)
+    np.testing.assert_array_equal(out, R.denormalize_f32(y.cpu().numpy()).reshape(n, -1, 2))
+    yb = model(x).cpu().numpy()
+    assert np.abs(R.denormalize_f32(yb).reshape(n, -1, 2) - out).max() <= 0.05
+    y64 = R.run(synth.synthetic_state_dict(0), x.cpu().numpy(), torch.float64)
+    px64 = R.denormalize_f32(y64.astype(np.float32)).reshape(n, -1, 2)
+    assert np.sqrt(((out - px64) ** 2).sum(-1)).max() <= 0.1  # px-L2, the fp16 budget (test_detector_gpu.FP16_PX_MAX)
