@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--precision fp16]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+Without a launcher (no WORLD_SIZE in the environment) and N > 1, this process starts the N
+ranks itself -- torchrun as a child process, before anything here touches the GPU (the
+reference's own multi-process launch is mp.spawn, perseus/detector/train.py:371-375) -- and
+exits with its status.  Every rank checks that the process group has N ranks.
+
 One step = one KeypointCNN forward (perseus/detector/models.py:34-40) over a batch of 64
 synthetic 256x256 RGBD frames already resident in HBM (BASELINE.json configs[1]).  At
 N > 1 each rank runs its own frame shard (weak scaling, weights replicated) and the
@@ -15,7 +20,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -53,7 +60,40 @@ def parse():
     p.add_argument("--no-streaming", action="store_true")
     p.add_argument("--stream-ticks", type=int, default=300, help="configs[4]: paced ticks per streaming mode")
     p.add_argument("--stream-window", type=int, default=24, help="configs[4]: pose-stage window (frames per camera)")
+    p.add_argument("--launcher-check", action="store_true",
+                   help="CPU-only rehearsal of the N-rank launch: every rank joins a gloo group, checks its size "
+                        "and rank 0 prints the ranks that joined (no GPU work)")
     return p.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` with no launcher around it: run the same command line as N ranks
+    under torchrun (a child process; this parent never initialises HIP, so no GPU state is
+    inherited or exec'd over) and return its exit status."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:  # a free rendezvous port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def launcher_check(args, world, rank):
+    """--launcher-check: the rank processes join a gloo group of --gpus ranks (CPU only)."""
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    n = dist.get_world_size()
+    if n != args.gpus:
+        raise SystemExit(f"rank {rank}: process group has {n} ranks, --gpus {args.gpus}")
+    t = torch.tensor([1 << rank], dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launcher_check": True, "n_gpus": n, "world_env": world, "ranks_mask": int(t.item())}))
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def main():
@@ -65,15 +105,22 @@ def main():
     from perseus_amd import shard, synth
     from perseus_amd.detector import KeypointCNN
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))  # before any GPU call in this process
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}: run `bench.py --gpus N` alone or under a "
+                         f"launcher of N ranks")
+    if args.launcher_check:
+        return launcher_check(args, world, rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"rank {rank}: RCCL group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     B = args.batch
     state = synth.synthetic_state_dict(args.seed)
@@ -152,7 +199,7 @@ def main():
             "metric": "RGBD frames/sec/GPU (256x256, batch 64); keypoint px-L2 vs CPU ref",
             "value": round(value, 1),
             "unit": "frames/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if world > 1 else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -279,19 +326,26 @@ def trajset_leg(model, x, args, dev, world, rank, reps=3):
             "timing": f"wall clock, barrier + synchronize, max over ranks, median of {reps}"}
 
 
-def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pose", "pixels")):
+def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pose", "pose_parity", "pixels")):
     """configs[4]: 3 x 720p RGBD cameras paced at `hz`, one StreamingPipeline tick per
     camera period (pinned host staging of the centre crops, one hipGraph replay: H2D,
     fused-preprocess forward at B = cams, denormalize, D2H pixels; mode "pose" adds the
     pose stage over a `window`-frame fixed-lag window per camera: advance, linearize the
-    reference's factors, one GN step, retract, D2H poses).  Latency = host time from the
-    start of staging to results on the host, p50 / p99 / max over `ticks` paced ticks
-    (mode "pixels": ticks // 3); device_ms = one replay between HIP events on the
-    pipeline's stream (20 back to back)."""
+    reference's factors, one GN step, retract, D2H poses; "pose_parity" is the same tick
+    with the detector in fp16x3, the mode that meets north_star's 1e-3 px, in its latency
+    mode).  Latency = host time from the start of staging to results on the host, p50 / p99
+    / max over `ticks` paced ticks (mode "pixels": ticks // 3); device_ms = one replay
+    between HIP events on the pipeline's stream (20 back to back)."""
     import numpy as np
     import torch
 
+    from perseus_amd.detector import KeypointCNN
     from perseus_amd.streaming import StreamingPipeline
+
+    parity = None
+    if "pose_parity" in modes:  # the same weights in the parity-grade precision
+        parity = KeypointCNN(num_channels=4, precision="fp16x3")
+        parity.load_state_dict(model.state_dict())
 
     rng = np.random.default_rng(0)
     n_src = 8  # rotate through a few distinct synthetic camera ticks
@@ -300,11 +354,12 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pos
     res = {"workload": f"configs[4]: {cams} x 720p RGBD @ {hz:g} Hz, centre crop 256, B = {cams} per tick",
            "unit": "ms", "timing": "host time from staging start to results on the host, paced ticks"}
     for mode in modes:
-        kw = dict(pose_window=window, proj_sigma=40.0) if mode == "pose" else {}
-        pipe = StreamingPipeline(model, n_cams=cams, graph=True, host_crop=True, device=dev, **kw)
+        kw = dict(pose_window=window, proj_sigma=40.0) if mode.startswith("pose") else {}
+        pipe = StreamingPipeline(parity if mode == "pose_parity" else model, n_cams=cams, graph=True, host_crop=True,
+                                 device=dev, **kw)
         for i in range(10):
             pipe(rgbs[i % n_src], deps[i % n_src])
-        n = ticks if mode == "pose" else max(ticks // 3, 30)
+        n = ticks if mode.startswith("pose") else max(ticks // 3, 30)
         lat = []
         period = 1.0 / hz
         t_next = time.perf_counter()
@@ -327,10 +382,11 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pos
         r = {"ticks": n, "p50_ms": round(float(np.percentile(lat, 50)), 4),
              "p99_ms": round(float(np.percentile(lat, 99)), 4), "max_ms": round(float(lat.max()), 4),
              "device_ms_per_tick": round(e0.elapsed_time(e1) / 20, 4)}
-        if mode == "pose":
+        if mode.startswith("pose"):
             r["window_frames"] = window
-            r["stage"] = ("forward_rgbd_px (split-K latency mode) + pa_window_advance + pa_trajectory_linearize + "
-                          "pa_trajectory_gn_step + pa_window_retract")
+            r["precision"] = pipe.model.precision
+            r["stage"] = ("forward_rgbd_px (latency mode) + pa_window_advance_n + pa_trajectory_linearize + "
+                          "pa_trajectory_gn_step (delta + info) + pa_window_retract_newest")
             r["solved_last_tick"] = int((pipe.info_h.numpy() == 0).sum())
         res[mode] = r
         pipe.close()

@@ -66,12 +66,13 @@ int pa_detector_reserve(pa_detector* d, int max_batch);
 int pa_detector_set_precision(pa_detector* d, int precision);
 
 /* Latency mode for small batches (the streaming pose stage, streaming.py:101-166: one
- * frame per camera per tick).  fp16 forwards of B <= max_batch frames run the convs of
- * layers 2-4 as split-K launches + a fixed-order reduce (layer2's stride-2 entry, with
+ * frame per camera per tick).  fp16 and fp16x3 forwards whose whole batch is
+ * B <= max_batch frames run the stem on short bands, layer1 on small tiles and the convs
+ * of layers 2-4 as split-K launches + a fixed-order reduce (layer2's stride-2 entry, with
  * 64 input channels, on one-tile workgroups instead), which fills the chip at a few
- * frames (deterministic, but not bit-identical to the batched kernels: the
- * f32 sums are taken in another order).  Allocates max_batch MiB of partials.
- * max_batch = 0 (default) turns it off; at most 64. */
+ * frames (deterministic, but not bit-identical to the batched kernels: the f32 sums are
+ * taken in another order; fp16x3 stays within its 1e-3 px parity bar).  Allocates
+ * max_batch MiB of partials.  max_batch = 0 (default) turns it off; at most 64. */
 int pa_detector_set_split_k(pa_detector* d, int max_batch);
 
 /* Replaces KeypointCNN.forward (models.py:34-40): x (B,C,H,W) f32 NCHW contiguous
@@ -79,12 +80,13 @@ int pa_detector_set_split_k(pa_detector* d, int max_batch);
  * normalized image coordinates.  B = 0 is a no-op. */
 int pa_detector_forward(pa_detector* d, const float* x_dev, int B, float* y_dev, void* stream);
 
-/* Camera frames -> keypoints in one pass: uint8 HWC RGB (bgr != 0: BGR
- * byte order, as the ZED delivers) + f32 depth in metres, both [B][Hs][Ws], centre-cropped
- * to 256x256; pa_preprocess_rgbd's arithmetic (streaming.py:68-80, deterministic near/far
- * clip, < 0 = off) is applied inside the stem's row loads, so the f32 (B,4,256,256) input
- * is never written.  Output bit-identical to pa_preprocess_rgbd + pa_detector_forward.
- * fp16 precision and 4-channel models only (PA_EINVAL otherwise). */
+/* Camera frames -> keypoints: uint8 HWC RGB (bgr != 0: BGR byte order, as
+ * the ZED delivers) + f32 depth in metres, both [B][Hs][Ws], centre-cropped to 256x256;
+ * pa_preprocess_rgbd's arithmetic (streaming.py:68-80, deterministic near/far clip, < 0 =
+ * off).  fp16: applied inside the stem's row loads, so the f32 (B,4,256,256) input is never
+ * written; fp16x3 / fp32: the preprocess kernel into the handle's own f32 staging (allocated
+ * by the first call of a batch size, outside any graph), then the forward.  Output
+ * bit-identical to pa_preprocess_rgbd + pa_detector_forward.  4-channel models only. */
 int pa_detector_forward_rgbd(pa_detector* d, const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws,
                              int bgr, float near_m, float far_m, float* y_dev, void* stream);
 
@@ -173,7 +175,11 @@ int pa_cv_linearize(int n, const double* v1_dev, const double* v2_dev, const dou
  * trajectory: one PoseDynamicsFactor (pose[f], angvel[f], vel[f], pose[f+1]) and
  * one ConstantVelocityFactor (vel[f], vel[f+1]).  Outputs use the per-factor
  * layouts of the batched entry points above; proj arrays have T*L*K rows, dyn
- * and cv arrays T*(L-1).  inv_sigma / err / J / status pointers may be NULL. */
+ * and cv arrays T*(L-1).  inv_sigma / err / J / status pointers may be NULL.
+ * nvalid (may be NULL): per trajectory the number of trailing frames that hold a real
+ * measurement (the streaming window before it has filled, pa_window_advance_n); the
+ * projection factors of frames l < L - nvalid[t] get status 2 and r = J = err = 0, so the
+ * GN step skips them. */
 typedef struct pa_traj_args {
   int T, L, n_kp, H, W;
   const float* y;          /* (T*L, 2K) normalized keypoints */
@@ -192,6 +198,7 @@ typedef struct pa_traj_args {
   int32_t* status;
   double *r_dyn, *j_dyn0, *j_dyn1, *j_dyn2, *j_dyn3, *err_dyn;
   double *r_cv, *j_cv0, *j_cv1, *err_cv;
+  const int32_t* nvalid;   /* (T) or NULL: frames with measurements, from the window's end */
 } pa_traj_args;
 
 int pa_trajectory_linearize(const pa_traj_args* args, void* stream);
@@ -204,8 +211,11 @@ int pa_trajectory_linearize(const pa_traj_args* args, void* stream);
  * solves (J^T J + lambda I) delta = -J^T r.  Outputs: D (T*L, 12, 12) diagonal and
  * E (T*(L-1), 12, 12) off-diagonal blocks of J^T J (E_l couples frame l rows with
  * frame l+1 columns), g (T*L, 12) = J^T r, delta (T*L, 12), info (T) = 0 or the
- * 1-based frame whose pivot block was not positive definite (delta NaN).  Projection
- * factors with status != 0 (cheirality) are skipped.  ws: pa_trajectory_gn_workspace. */
+ * 1-based frame whose pivot block was not positive definite (delta NaN).  D, E and g
+ * may all be NULL (then the blocks stay on chip: the step's HBM traffic is the factors in
+ * and delta out).  Projection factors with status != 0 (cheirality, or a frame outside a
+ * window's filled part) are skipped; with n_kp = 0 r_proj / j_proj may be NULL.
+ * ws: pa_trajectory_gn_workspace. */
 size_t pa_trajectory_gn_workspace(int T, int L);
 int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const double* j_proj,
                           const int32_t* status_proj, const double* r_dyn, const double* j_dyn0,
@@ -226,6 +236,11 @@ int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const do
  * trajectories with info[t] != 0 are left unchanged (info may be NULL). */
 int pa_window_advance(int T, int L, int n_kp, const float* y_new_dev, float* y_dev, double* pose_dev,
                       double* angvel_dev, double* vel_dev, double dt, int vel_frame, void* stream);
+/* pa_window_advance that also counts the window's real frames: nvalid_dev (T) int32 += 1 up
+ * to L per advance (zero it with the window's reset; pa_traj_args.nvalid reads it). */
+int pa_window_advance_n(int T, int L, int n_kp, const float* y_new_dev, float* y_dev, double* pose_dev,
+                        double* angvel_dev, double* vel_dev, int32_t* nvalid_dev, double dt, int vel_frame,
+                        void* stream);
 int pa_window_retract(int T, int L, const double* delta_dev, const int32_t* info_dev, double* pose_dev,
                       double* angvel_dev, double* vel_dev, void* stream);
 /* pa_window_retract that also writes each trajectory's newest (last-frame) pose after the

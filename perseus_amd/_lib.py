@@ -31,7 +31,7 @@ class TrajArgs(C.Structure):
                 ("isig_cv", C.c_void_p), ("r_proj", C.c_void_p), ("j_proj", C.c_void_p), ("err_proj", C.c_void_p),
                 ("status", C.c_void_p), ("r_dyn", C.c_void_p), ("j_dyn0", C.c_void_p), ("j_dyn1", C.c_void_p),
                 ("j_dyn2", C.c_void_p), ("j_dyn3", C.c_void_p), ("err_dyn", C.c_void_p), ("r_cv", C.c_void_p),
-                ("j_cv0", C.c_void_p), ("j_cv1", C.c_void_p), ("err_cv", C.c_void_p)]
+                ("j_cv0", C.c_void_p), ("j_cv1", C.c_void_p), ("err_cv", C.c_void_p), ("nvalid", C.c_void_p)]
 
 
 # name -> (restype, argtypes)
@@ -67,6 +67,8 @@ _SIGS = {
                               + [C.c_void_p] * 6 + [C.c_size_t, C.c_void_p]),
     "pa_window_advance": (C.c_int, [C.c_int, C.c_int, C.c_int] + [C.c_void_p] * 5 + [C.c_double, C.c_int,
                                                                                      C.c_void_p]),
+    "pa_window_advance_n": (C.c_int, [C.c_int, C.c_int, C.c_int] + [C.c_void_p] * 6 + [C.c_double, C.c_int,
+                                                                                       C.c_void_p]),
     "pa_window_retract": (C.c_int, [C.c_int, C.c_int] + [C.c_void_p] * 6),
     "pa_debug_gn_set_assemblers": (C.c_int, [C.c_int]),
     "pa_window_retract_newest": (C.c_int, [C.c_int, C.c_int] + [C.c_void_p] * 7),

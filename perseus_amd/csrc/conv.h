@@ -101,6 +101,11 @@ int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s, bool split_l2 = fals
 // the conv and the downsample reduced in one pass (layer3's batched kernel is kept)
 int launch_conv3x3s2_small(const ConvS2Args& a, hipStream_t s, const char** kname);
 size_t splitk_part_floats(int B);
+// fp16x3 latency mode: the X3 forms (conv_splitk.hip; same partials buffer)
+int launch_conv3x3_splitk_x3(const ConvArgs& a, hipStream_t s, const char** kname);
+int launch_conv3x3s2_small_x3(const ConvS2Args& a, hipStream_t s, const char** kname);
+int launch_stem_pool_x3_small(const float* x, int B, int Cin, const _Float16* w, const float* bias_s,
+                              const float* scale, _Float16* out, hipStream_t s);
 
 // layer1 (Cin = Cout = 64), fp16: weight-resident persistent kernel (conv_c64.hip)
 int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s);
@@ -134,8 +139,9 @@ int launch_conv3x3_x3_l2(const ConvArgs& a, hipStream_t s);
 int launch_conv3x3_x3_l3(const ConvArgs& a, hipStream_t s);
 int launch_conv3x3_x3_l4(const ConvArgs& a, hipStream_t s);
 int launch_conv3x3s2_x3(const ConvS2Args& a, hipStream_t s, const char** kname);
+// px (optional): the keypoints also denormalized to an H x W image (launch_postprocess's values)
 int launch_head_x3(const _Float16* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
-                   hipStream_t s);
+                   hipStream_t s, float* px = nullptr, int H = 0, int W = 0);
 
 template <typename T>
 int launch_maxpool(const T* in, int B, int H, int W, int C, T* out, hipStream_t s);

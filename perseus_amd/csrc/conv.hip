@@ -570,9 +570,11 @@ __global__ __launch_bounds__(256) void head_fp16(const _Float16* __restrict__ in
 
 // fp16x3 parity mode: head_fp16's arithmetic on the f32 values hi + lo of the layer4
 // output's plane pair ([hi (512) | lo (512)] per pixel; hi + lo is exact in f32).
+// px (optional): the keypoints also denormalized (postprocess_kernel's arithmetic), as head_fp16
 template <int NOUT>
 __global__ __launch_bounds__(256) void head_x3(const _Float16* __restrict__ in, const float* __restrict__ fcw,
-                                               const float* __restrict__ fcb, float* __restrict__ y) {
+                                               const float* __restrict__ fcb, float* __restrict__ y,
+                                               float* __restrict__ px, int H, int W) {
   constexpr int HW = 64, C = 512;
   __shared__ float csum[4][C];
   __shared__ float part[4][NOUT];
@@ -612,16 +614,20 @@ __global__ __launch_bounds__(256) void head_x3(const _Float16* __restrict__ in, 
     if (lane == 0) part[wid][j] = v;
   }
   __syncthreads();
-  if (tid < NOUT) y[(size_t)n * NOUT + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + fcb[tid];
+  if (tid < NOUT) {
+    const float v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid] + fcb[tid];
+    y[(size_t)n * NOUT + tid] = v;
+    if (px) px[(size_t)n * NOUT + tid] = kornia_denorm(v, (tid & 1) ? H : W);
+  }
 }
 
 int launch_head_x3(const _Float16* in, int B, int HW, int C, const float* fcw, const float* fcb, int nout, float* y,
-                   hipStream_t s) {
+                   hipStream_t s, float* px, int H, int W) {
   PA_CHECK(HW == 64 && C == 512 && nout >= 1 && nout <= 32, "head x3: HW=%d C=%d nout=%d", HW, C, nout);
   if (B <= 0) return PA_OK;
   switch (nout) {
 #define PA_HX3(N) \
-  case N: hipLaunchKernelGGL(head_x3<N>, dim3(B), dim3(256), 0, s, in, fcw, fcb, y); break;
+  case N: hipLaunchKernelGGL(head_x3<N>, dim3(B), dim3(256), 0, s, in, fcw, fcb, y, px, H, W); break;
     PA_HX3(2) PA_HX3(4) PA_HX3(6) PA_HX3(8) PA_HX3(10) PA_HX3(12) PA_HX3(14) PA_HX3(16) PA_HX3(18) PA_HX3(20)
     PA_HX3(22) PA_HX3(24) PA_HX3(26) PA_HX3(28) PA_HX3(30) PA_HX3(32)
 #undef PA_HX3

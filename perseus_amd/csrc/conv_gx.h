@@ -249,6 +249,14 @@ struct GxBlocks {
   static constexpr int wblk2(int vb) { return NCB + vb / 2; }
 };
 
+// element offset of 64-channel block b within one pixel / weight tap of a conv whose
+// activation / weight planes hold CF channels each: [hi (CF) | lo (CF)]; X3 blocks
+// b >= NCB (this launch's channels per plane / 64) are the lo plane's
+template <int NCB, int CF>
+__device__ __forceinline__ constexpr int gx_boff(int b) {
+  return b < NCB ? b * 64 : CF + (b - NCB) * 64;
+}
+
 // hi / lo fp16 pair of an f32 value (hi + lo == v to 2^-22 relative)
 struct HiLo {
   _Float16 hi, lo;
@@ -272,12 +280,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
   static_assert(!XM || (X3 && FD == 1), "merged X3 steps: fp16x3, fragments half a step ahead");
-  static_assert(!PART || (!X3 && EPI == 0), "split-K partials: fp16, no epilogue");
+  static_assert(!PART || EPI == 0, "split-K partials: no epilogue");
   using VB = GxBlocks<X3, NCB, XM>;
   constexpr int XS = X3 ? 2 : 1;  // fp16 planes per activation / weight element
   constexpr int NSTEPS = VB::NVB * 9;
-  constexpr int KW = XS * CIN;  // weight elements per tap
-  constexpr int KTOT = 9 * KW;
   static_assert(!(X3 && (EPI & EPI_HEAD)), "fused head: fp16 path only");
   constexpr int PH = TH + 2, PW = TW + 2;
   constexpr int IMS = (TW == 8) ? ((PH * PW + 7) / 16 * 16 + 8) : PH * PW;
@@ -314,7 +320,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   const int H = a.Hout, W = a.Wout;
   // PART: pixel stride and weight tap stride are the full conv's a.Cin; split blockIdx.y
   // starts at input channel CIN * blockIdx.y
-  const int kin = PART ? a.Cin : KW;
+  // CF = the full conv's input channels per plane (PART: NS * CIN, a.Cin); KIN = pixel /
+  // weight-tap stride in elements; boff(b) = element offset of 64-channel block b of the
+  // [hi (CF) | lo (CF)] planes within a pixel or tap (X3 blocks >= NCB are the lo plane's)
+  constexpr int CF = PART ? PART * CIN : CIN;
+  constexpr int kin = XS * CF;
   const int kc0 = PART ? CIN * (int)blockIdx.y : 0;
   const _Float16* __restrict__ in = (const _Float16*)a.in + kc0;
   const _Float16* __restrict__ w = (const _Float16*)a.w + kc0;
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   auto dma_patch = [&](int vb, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PDMA; ++i) {
-      const char* s = psrc[i] ? psrc[i] + VB::pblk(vb) * 128 : (const char*)gx_zero_line;
+      const char* s = psrc[i] ? psrc[i] + gx_boff<NCB, CF>(VB::pblk(vb)) * 2 : (const char*)gx_zero_line;
       xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
     }
   };
@@ -370,17 +380,18 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   for (int i = 0; i < WDMA; ++i) {
     const int c = (i * NW + wid) * 64 + lane;
     const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
-    wsrc[i] = w + (size_t)(n0 + xperm(co)) * (PART ? 9 * kin : KTOT) + lc * 8;
+    wsrc[i] = w + (size_t)(n0 + xperm(co)) * (9 * kin) + lc * 8;
   }
   auto dma_w = [&](int s) __attribute__((always_inline)) {
     const int vb = s / 9, tap = s % 9;
 #pragma unroll
     for (int i = 0; i < WDMA; ++i)
-      xdma16(wsrc[i] + tap * kin + VB::wblk(vb) * 64, wring + (s % NSLOT) * WSLOT + (i * NW + wid) * 1024);
+      xdma16(wsrc[i] + tap * kin + gx_boff<NCB, CF>(VB::wblk(vb)), wring + (s % NSLOT) * WSLOT + (i * NW + wid) * 1024);
     if (VB::two(vb))  // compile-time after inlining (s is a step constant)
 #pragma unroll
       for (int i = 0; i < WDMA; ++i)
-        xdma16(wsrc[i] + tap * kin + VB::wblk2(vb) * 64, wring + (s % NSLOT) * WSLOT + WB + (i * NW + wid) * 1024);
+        xdma16(wsrc[i] + tap * kin + gx_boff<NCB, CF>(VB::wblk2(vb)),
+               wring + (s % NSLOT) * WSLOT + WB + (i * NW + wid) * 1024);
   };
 
   const int o = xfrag(r16);
@@ -542,7 +553,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
       if (!ok[tm]) continue;
-      const size_t pix = pixo[tm] / Cout;  // (n * H + y) * W + x (XS = 1: pixo = pix * Cout + channel < Cout)
+      const size_t pix = pixo[tm] / (XS * Cout);  // (n * H + y) * W + x (pixo = pix * XS * Cout + channel < Cout)
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         const int c = n0 + wn * WTN + (tn >> 1) * 32 + q * 8 + (tn & 1) * 4;
@@ -584,13 +595,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
 }
 
 // split-K partial launch (PART = NS): grid.y = NS splits of CIN channels, f32 partials to a.part
-template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int NS>
+// (X3: the partial sums of the three products, still scaled by 2^e; the reduce unscales)
+template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int NS, bool X3 = false, bool XM = false>
 static int run_gx_part(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.part && a.Cin == NS * CIN && a.Hout == a.Hin && a.Hout % TH == 0 && a.Wout % TW == 0 && a.Cout % BN == 0,
            "gx split-K: Cin %d Cout %d %dx%d", a.Cin, a.Cout, a.Hout, a.Wout);
   const int ntn = a.Cout / BN;
   const int nsp = ((a.B + NI - 1) / NI) * (a.Hout / TH) * (a.Wout / TW);
-  hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, 1, 0, 0, 1, true, false, false, NS>), dim3(nsp * ntn, NS),
+  hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, 1, 0, 0, 1, true, X3, XM, NS>), dim3(nsp * ntn, NS),
                      dim3(WM * WN * 64), 0, s, a, 0);
   PA_LAUNCH_CHECK();
   return PA_OK;

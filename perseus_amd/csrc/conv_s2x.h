@@ -52,8 +52,6 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   constexpr int SPT = VB::NVB * SPB;  // steps per tile
   constexpr int NBLK = TPW * VB::NVB;  // patch blocks in the stream
   constexpr int NSTEPS = TPW * SPT;
-  constexpr int KW = XS * CIN;
-  constexpr int KTOT = 9 * KW;
   constexpr int PH = 2 * TH + 1;
   constexpr int PW = TW == 8 ? 20 : 2 * TW + 1;  // LDS positions per patch row
   constexpr int NP = PH * PW;
@@ -71,7 +69,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile");
   static_assert(G >= 1 && G <= 3 && PD >= G + 1 && PD <= 8, "prefetch distance / steps per barrier");
   constexpr int NSLOT = PD + G;
-  static_assert(!PART || (TPW == 1 && !X3), "split-K partials: fp16, one tile per workgroup");
+  static_assert(!PART || TPW == 1, "split-K partials: one tile per workgroup");
   constexpr int RL = (TPW > 1 || PART) ? 0 : 2 * XS * TN;  // epilogue loads in the stream: bias, bias2 (+ scale, scale2)
   constexpr int RSD = 4;
   constexpr int NST = TM * (TN / 2) * 2 * XS;  // output stores per tile (out, out2; hi, lo)
@@ -88,7 +86,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   const int H = a.Hout, W = a.Wout, Hin = a.Hin, Win = a.Win, Cout = a.Cout;
   // PART: pixel and tap strides are the full conv's a.Cin; split blockIdx.y starts at input
   // channel CIN * blockIdx.y
-  const int kin = PART ? a.Cin : KW;
+  // as conv_gx.h: CF = the full conv's channels per plane, kin = pixel / tap stride,
+  // gx_boff = a 64-channel block's offset in the [hi (CF) | lo (CF)] planes
+  constexpr int CF = PART ? PART * CIN : CIN;
+  constexpr int kin = XS * CF;
   const int kc0 = PART ? CIN * (int)blockIdx.y : 0;
   const _Float16* __restrict__ in = (const _Float16*)a.in + kc0;
   const _Float16* __restrict__ w = (const _Float16*)a.w + kc0;
@@ -130,7 +131,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
       const int col = pos <= TW ? 2 * pos : 2 * (pos - TW - 1) + 1;
       const int h = 2 * th0 - 1 + pr, x = 2 * tw0 - 1 + col;
       const bool ok = p < NP && pos < 2 * TW + 1 && (unsigned)h < (unsigned)Hin && (unsigned)x < (unsigned)Win;
-      const char* s = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * kin + lc * 8) + VB::pblk(vb) * 128
+      const char* s = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * kin + lc * 8 +
+                                         gx_boff<NCB, CF>(VB::pblk(vb)))
                          : (const char*)gx_zero_line;
       xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
     }
@@ -142,12 +144,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   for (int i = 0; i < WDMA; ++i) {
     const int c = (i * NW + wid) * 64 + lane;
     const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
-    wsrc[i] = w + (size_t)(n0 + xperm(co)) * (PART ? 9 * kin : KTOT) + lc * 8;
+    wsrc[i] = w + (size_t)(n0 + xperm(co)) * (9 * kin) + lc * 8;
     dsrc[i] = wds + (size_t)(n0 + xperm(co)) * kin + lc * 8;
   }
   auto dma_w = [&](int s) __attribute__((always_inline)) {
     const int vb = (s % SPT) / SPB, t = s % SPB;
-    const int wb = VB::wblk(vb) * 64;
+    const int wb = gx_boff<NCB, CF>(VB::wblk(vb));
 #pragma unroll
     for (int i = 0; i < WDMA; ++i) {
       const _Float16* src = t < 9 ? wsrc[i] + t * kin + wb : dsrc[i] + wb;
@@ -352,14 +354,14 @@ static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
 }
 
 // split-K partial launch (PART = NS): grid.y = NS splits of CIN channels, f32 partials to a.part
-template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int NS>
+template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int NS, bool X3 = false>
 static int run_s2x_part(const ConvS2Args& a, hipStream_t s) {
   PA_CHECK(a.part && a.Cin == NS * CIN && a.Hin == 2 * a.Hout && a.Win == 2 * a.Wout && a.Hout % TH == 0 &&
                a.Wout % TW == 0 && a.Cout % BN == 0,
            "s2x split-K: Cin %d Cout %d %dx%d", a.Cin, a.Cout, a.Hout, a.Wout);
   const int ntn = a.Cout / BN;
   const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW);
-  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, 1, true, false, 0, 1, NS>), dim3(nsp * ntn, NS),
+  hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, 1, true, X3, 0, 1, NS>), dim3(nsp * ntn, NS),
                      dim3(WM * WN * 64), 0, s, a, 0);
   PA_LAUNCH_CHECK();
   return PA_OK;

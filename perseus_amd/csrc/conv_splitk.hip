@@ -108,6 +108,127 @@ int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s, bool split_l2) {
                        (const _Float16*)((a.epi & EPI_RES) ? a.res : nullptr), (_Float16*)a.out, a.Cout, nullptr, nullptr, s);
 }
 
+// fp16x3 (conv_gx.h X3): out[p] = the (hi, lo) plane pair of relu(sum_s part[s][p][c] *
+// scale[c] + bias[c] (+ res_hi + res_lo)), the batched X3 epilogue's operations on the
+// split-order sum (the partials carry the weights' 2^e; the unscale is exact).  out / res
+// are [pixel][hi (Cout) | lo (Cout)]; with out2 (stride-2 entry) the second partial set is
+// the downsample: sum * scale2 + bias2, no ReLU.
+__global__ __launch_bounds__(256) void splitk_reduce_x3(const float* __restrict__ part, int nsplit, unsigned n,
+                                                        const float* __restrict__ bias, const float* __restrict__ scale,
+                                                        const _Float16* __restrict__ res, _Float16* __restrict__ out,
+                                                        int Cout, const float* __restrict__ bias2,
+                                                        const float* __restrict__ scale2, _Float16* __restrict__ out2) {
+  unsigned e = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const bool second = e >= n;
+  if (second) {
+    e -= n;
+    if (!out2 || e >= n) return;
+    part += (size_t)nsplit * n;
+    bias = bias2;
+    scale = scale2;
+    out = out2;
+    res = nullptr;
+  }
+  const unsigned pix = e / (unsigned)Cout;
+  const int c = (int)(e - pix * (unsigned)Cout);
+  f32x4 lo = *reinterpret_cast<const f32x4*>(part + e), hi = *reinterpret_cast<const f32x4*>(part + e + 4);
+  for (int s = 1; s < nsplit; ++s) {
+    lo += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e);
+    hi += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e + 4);
+  }
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + c), b1 = *reinterpret_cast<const f32x4*>(bias + c + 4);
+  const f32x4 s0 = *reinterpret_cast<const f32x4*>(scale + c), s1 = *reinterpret_cast<const f32x4*>(scale + c + 4);
+  const size_t o = (size_t)pix * 2 * Cout + c;
+  half8 rh{}, rl{};
+  if (res) {
+    rh = *reinterpret_cast<const half8*>(res + o);
+    rl = *reinterpret_cast<const half8*>(res + o + Cout);
+  }
+  half8 oh, ol;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = (j < 4 ? lo[j] : hi[j - 4]) * (j < 4 ? s0[j] : s1[j - 4]) + (j < 4 ? b0[j] : b1[j - 4]);
+    if (res) v += (float)rh[j] + (float)rl[j];
+    const HiLo hl = split_x3(second ? v : fmaxf(v, 0.f));
+    oh[j] = hl.hi;
+    ol[j] = hl.lo;
+  }
+  *reinterpret_cast<half8*>(out + o) = oh;
+  *reinterpret_cast<half8*>(out + o + Cout) = ol;
+}
+
+static int launch_reduce_x3(const float* part, int nsplit, size_t n, const float* bias, const float* scale,
+                            const _Float16* res, _Float16* out, int Cout, const float* bias2, const float* scale2,
+                            _Float16* out2, hipStream_t s) {
+  PA_CHECK(n % 8 == 0 && n < 0x40000000u && Cout % 8 == 0 && scale && (!out2 || scale2),
+           "split-K reduce (fp16x3): %zu elements", n);
+  const size_t threads = (out2 ? 2 * n : n) / 8;
+  hipLaunchKernelGGL(splitk_reduce_x3, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, part, nsplit,
+                     (unsigned)n, bias, scale, res, out, Cout, bias2, scale2, out2);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+// fp16x3 latency mode (the parity-grade streaming tick): the X3 forms of the convs above on
+// small tiles, layers 2-4 split-K over the 64-channel input blocks (the merged x_hi steps,
+// conv_gx.h XM, in every split) + splitk_reduce_x3.  Not bit-identical to the batched X3
+// kernels (another f32 summation order); both stay within the 1e-3 px parity bar.
+int launch_conv3x3_splitk_x3(const ConvArgs& a, hipStream_t s, const char** kname) {
+  PA_CHECK(a.stride == 1 && a.pad == 1 && (a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES)) && a.scale,
+           "split-K conv (fp16x3): stride-1, relu (+residual), scale required (epi %d)", a.epi);
+  PA_CHECK(a.B <= 64, "split-K conv: batch %d above 64", a.B);
+  if (a.B <= 0) return PA_OK;
+  int rc;
+  if (a.Cin == 64 && a.Cout == 64 && a.Hout == 64 && a.Wout == 64) {
+    // layer1: one 64-channel block, nothing to split; 8 x 16 tiles (4 waves, 18 merged steps)
+    if (kname) *kname = "conv3x3x3_l1_small";
+    return run_gx<8, 16, 1, 64, 2, 2, 64, 3, 1, 0, 1, true, true, true>(a, false, s);
+  }
+  if (a.Cin == 128 && a.Cout == 128 && a.Hout == 32 && a.Wout == 32) {
+    if (kname) *kname = "conv3x3x3_l2_splitk";
+    rc = run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 2, true, true>(a, s);
+  } else if (a.Cin == 256 && a.Cout == 256 && a.Hout == 16 && a.Wout == 16) {
+    if (kname) *kname = "conv3x3x3_l3_splitk";
+    rc = run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 4, true, true>(a, s);
+  } else if (a.Cin == 512 && a.Cout == 512 && a.Hout == 8 && a.Wout == 8) {
+    if (kname) *kname = "conv3x3x3_l4_splitk";
+    rc = run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8, true, true>(a, s);
+  } else {
+    set_error("split-K conv (fp16x3): no configuration for %dx%d x %d -> %d", a.Hout, a.Wout, a.Cin, a.Cout);
+    return PA_EINVAL;
+  }
+  if (rc != PA_OK) return rc;
+  return launch_reduce_x3(a.part, a.Cin / 64, (size_t)a.B * a.Hout * a.Wout * a.Cout, a.bias, a.scale,
+                          (const _Float16*)((a.epi & EPI_RES) ? a.res : nullptr), (_Float16*)a.out, a.Cout, nullptr,
+                          nullptr, nullptr, s);
+}
+
+int launch_conv3x3s2_small_x3(const ConvS2Args& a, hipStream_t s, const char** kname) {
+  PA_CHECK(a.B <= 64, "split-K conv: batch %d above 64", a.B);
+  if (a.B <= 0) return PA_OK;
+  if (a.Hout == 32 && a.Cin == 64 && a.Cout == 128) {
+    // one input-channel block: unsplit, 64-channel tiles on 4 waves (B = 3: 96 workgroups of 30 steps)
+    if (kname) *kname = "conv3x3s2x3_l2_small";
+    return run_s2x<4, 16, 64, 2, 2, 64, 3, 1, true, true>(a, false, s);
+  }
+  int rc, ns;
+  if (a.Hout == 16 && a.Cin == 128 && a.Cout == 256) {
+    if (kname) *kname = "conv3x3s2x3_l3_splitk";
+    ns = 2;
+    rc = run_s2x_part<4, 16, 64, 2, 2, 64, 3, 2, true>(a, s);
+  } else if (a.Hout == 8 && a.Cin == 256 && a.Cout == 512) {
+    if (kname) *kname = "conv3x3s2x3_l4_splitk";
+    ns = 4;
+    rc = run_s2x_part<8, 8, 64, 2, 2, 64, 3, 4, true>(a, s);
+  } else {
+    set_error("s2x3 small batch: no configuration for %dx%d x %d -> %d", a.Hout, a.Wout, a.Cin, a.Cout);
+    return PA_EINVAL;
+  }
+  if (rc != PA_OK) return rc;
+  return launch_reduce_x3(a.part, ns, (size_t)a.B * a.Hout * a.Wout * a.Cout, a.bias, a.scale, nullptr,
+                          (_Float16*)a.out, a.Cout, a.bias2, a.scale2, (_Float16*)a.out2, s);
+}
+
 int launch_conv3x3s2_small(const ConvS2Args& a, hipStream_t s, const char** kname) {
   PA_CHECK(a.B <= 64, "split-K conv: batch %d above 64", a.B);
   if (a.B <= 0) return PA_OK;

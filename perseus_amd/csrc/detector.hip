@@ -62,6 +62,8 @@ struct pa_detector {
   unsigned long long* trace = nullptr;         // pa_detector_debug_set_trace
   int splitk_max = 0;                          // pa_detector_set_split_k: batches <= this run split-K
   float* part = nullptr;                       // its f32 partials (splitk_part_floats(splitk_max))
+  float* xin = nullptr;                        // forward_rgbd's f32 input staging (fp16x3 / fp32)
+  int xin_cap = 0;
 };
 
 namespace pa {
@@ -303,8 +305,10 @@ struct Prof {
     if (_rc != PA_OK) return _rc; \
   } while (0)
 
+// small: the latency mode (pa_detector_set_split_k), decided once per forward call from
+// the caller's whole batch (a chunk of a larger batch never switches to it)
 template <typename T>
-static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof,
+static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof, bool small,
                      const RgbdSrc* rgbd = nullptr, float* px = nullptr) {
   const T* wts = std::is_same<T, float>::value ? (const T*)d->w32 : (const T*)d->w16;
   T* S = reinterpret_cast<T*>(d->ws);
@@ -340,7 +344,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     if constexpr (std::is_same<T, _Float16>::value) {
       const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : a.Hout == 8 ? 4 : 0;
       // g_variant[layer] == 71 (A/B): layer2 split as well, layer1 on the persistent kernel
-      if (layer && B <= d->splitk_max && (g_variant[layer] == 0 || g_variant[layer] == 71) && !(a.epi & EPI_HEAD)) {
+      if (layer && small && (g_variant[layer] == 0 || g_variant[layer] == 71) && !(a.epi & EPI_HEAD)) {
         const bool split_l2 = g_variant[layer] == 71;
         static const char* names[5] = {"", "conv3x3x_l1_small", "conv3x3x_l2_small", "conv3x3x_l3_splitk",
                                        "conv3x3x_l4_splitk"};
@@ -384,9 +388,9 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       sa.Wout = ho;
       sa.Cout = c1.cout;
       sa.trace = trace();
-      bool small = false;
-      if constexpr (std::is_same<T, _Float16>::value) small = B <= d->splitk_max && g_variant[6] == 0 && ho != 16;
-      if (small) {
+      bool small_s2 = false;
+      if constexpr (std::is_same<T, _Float16>::value) small_s2 = small && g_variant[6] == 0 && ho != 16;
+      if (small_s2) {
         sa.part = d->part;
         PA_RUN(launch_conv3x3s2_small(sa, s, &kn), kn);
       } else {
@@ -486,15 +490,22 @@ constexpr int kChunk = 1024;
 // fp16x3 parity mode: every conv as 3 fp16 MFMA products of hi/lo planes,
 // f32 accumulate; same schedule and fusions as the fp16 path (stem + pool fused, stride-2
 // conv + downsample fused, in-place residual), separate head.
-static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof) {
+// small: the fp16x3 latency mode (short stem bands, small tiles, layers 2-4 split-K,
+// conv_splitk.hip); px (optional): the head also writes the denormalized pixels
+static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof, bool small,
+                      float* px = nullptr) {
   _Float16* X = reinterpret_cast<_Float16*>(d->ws);
   const size_t act_el = (size_t)B * 64 * 64 * 64 * 2;  // two planes
   _Float16* Tb = X + act_el;
   _Float16* D = Tb + act_el;
   if (prof) prof->mark("start");
   const ConvL& st = d->convs[0];
-  PA_RUN(launch_stem_pool_x3(x, B, d->in_ch, d->w3 + st.w3_off, d->bstem3, d->scl + st.b_off, X, s),
-         "stem_x3_conv7x7_pool");
+  if (small)
+    PA_RUN(launch_stem_pool_x3_small(x, B, d->in_ch, d->w3 + st.w3_off, d->bstem3, d->scl + st.b_off, X, s),
+           "stem_x3_conv7x7_pool_small");
+  else
+    PA_RUN(launch_stem_pool_x3(x, B, d->in_ch, d->w3 + st.w3_off, d->bstem3, d->scl + st.b_off, X, s),
+           "stem_x3_conv7x7_pool");
   int hw = 64;
   for (const Block& b : d->blocks) {
     const ConvL& c1 = d->convs[b.conv1];
@@ -503,7 +514,11 @@ static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream
     const char* kn = nullptr;
     const _Float16* res = X;
     _Float16* out = X;  // identity block: residual add in place (same element, same thread)
-    auto s1 = [&](const ConvArgs& a) -> int {
+    auto s1 = [&](ConvArgs& a) -> int {
+      if (small) {
+        a.part = d->part;
+        return launch_conv3x3_splitk_x3(a, s, &kn);
+      }
       switch (a.Hout) {
         case 64: kn = "conv3x3x3_l1"; return launch_conv3x3_x3_l1(a, s);
         case 32: kn = "conv3x3x3_l2"; return launch_conv3x3_x3_l2(a, s);
@@ -541,7 +556,11 @@ static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream
       sa.Hout = ho;
       sa.Wout = ho;
       sa.Cout = c1.cout;
-      PA_RUN(launch_conv3x3s2_x3(sa, s, &kn), kn);
+      sa.part = d->part;
+      if (small)
+        PA_RUN(launch_conv3x3s2_small_x3(sa, s, &kn), kn);
+      else
+        PA_RUN(launch_conv3x3s2_x3(sa, s, &kn), kn);
       res = D;
       out = D;
     } else {
@@ -571,50 +590,85 @@ static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
   }
-  PA_RUN(launch_head_x3(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s), "avgpool_fc_x3");
+  PA_RUN(launch_head_x3(X, B, hw * hw, 512, d->fcw, d->fcb, 2 * d->n_kp, y, s, px, d->H, d->W), "avgpool_fc_x3");
   return PA_OK;
 }
 
-static int forward(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof) {
+// the latency mode applies to the whole call (fp16 and fp16x3; fp32 has no such mode)
+static bool small_mode(const pa_detector* d, int B) { return B <= d->splitk_max && d->prec != PA_PREC_FP32; }
+
+// one chunk of frames (x: f32 NCHW) in the handle's precision
+static int forward_chunk(pa_detector* d, const float* x, int nb, float* y, hipStream_t s, Prof* prof, bool small,
+                         float* px) {
+  if (d->prec == PA_PREC_FP32) return forward_t<float>(d, x, nb, y, s, prof, false, nullptr, px);
+  if (d->prec == PA_PREC_FP16X3) return forward_x3(d, x, nb, y, s, prof, small, px);
+  return forward_t<_Float16>(d, x, nb, y, s, prof, small, nullptr, px);
+}
+
+static int forward(pa_detector* d, const float* x, int B, float* y, hipStream_t s, Prof* prof, float* px = nullptr) {
   PA_CHECK(d, "null detector");
   PA_CHECK(B >= 0, "batch %d", B);
   if (B == 0) return PA_OK;
   PA_CHECK(x && y, "null input/output pointer");
   PA_TRY(ensure_ws(d, B < kChunk ? B : kChunk));
   HandleScope hs(d);
+  const bool small = small_mode(d, B);
   const size_t in_frame = (size_t)d->in_ch * d->H * d->W, out_frame = 2 * (size_t)d->n_kp;
   for (int off = 0; off < B; off += kChunk) {
     const int nb = B - off < kChunk ? B - off : kChunk;
-    const float* xc = x + off * in_frame;
-    float* yc = y + off * out_frame;
-    const int rc = d->prec == PA_PREC_FP32     ? forward_t<float>(d, xc, nb, yc, s, prof)
-                   : d->prec == PA_PREC_FP16X3 ? forward_x3(d, xc, nb, yc, s, prof)
-                                               : forward_t<_Float16>(d, xc, nb, yc, s, prof);
+    const int rc = forward_chunk(d, x + off * in_frame, nb, y + off * out_frame, s, prof, small,
+                                 px ? px + off * out_frame : nullptr);
     if (rc != PA_OK) return rc;
   }
   return PA_OK;
 }
 
-// camera frames -> keypoints, preprocess fused into the stem (fp16, 4-channel models)
+// the f32 (B, 4, 256, 256) input of the non-fused RGBD path (fp16x3 / fp32), grown outside
+// any captured graph (the first call of a given batch size allocates)
+static int ensure_xin(pa_detector* d, int B) {
+  if (B <= d->xin_cap) return PA_OK;
+  if (d->xin) PA_HIP(hipFree(d->xin));
+  d->xin = nullptr;
+  d->xin_cap = 0;
+  if (hipMalloc(&d->xin, (size_t)B * 4 * 256 * 256 * sizeof(float)) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("forward_rgbd: input staging hipMalloc failed");
+    return PA_ENOMEM;
+  }
+  d->xin_cap = B;
+  return PA_OK;
+}
+
+// camera frames -> keypoints.  fp16: the preprocess is fused into the stem's row loads;
+// fp16x3 / fp32: pa_preprocess_rgbd's kernel into the handle's f32 staging, then the forward
+// (4-channel models)
 static int forward_rgbd(pa_detector* d, const RgbdSrc& src, int B, float* y, hipStream_t s, float* px = nullptr) {
   PA_CHECK(d, "null detector");
   PA_CHECK(B >= 0, "batch %d", B);
   if (B == 0) return PA_OK;
   PA_CHECK(src.rgb && src.depth && y, "null input/output pointer");
-  PA_CHECK(d->prec == PA_PREC_FP16, "forward_rgbd: fused preprocess is the fp16 path (fp32: pa_preprocess_rgbd + "
-                                    "pa_detector_forward)");
   PA_CHECK(d->in_ch == 4, "forward_rgbd: needs a 4-channel (RGBD) model, have %d", d->in_ch);
   PA_CHECK(src.Hs >= 256 && src.Ws >= 256, "forward_rgbd: source %dx%d smaller than 256x256", src.Hs, src.Ws);
   PA_TRY(ensure_ws(d, B < kChunk ? B : kChunk));
+  const bool fused = d->prec == PA_PREC_FP16;
+  if (!fused) PA_TRY(ensure_xin(d, B < kChunk ? B : kChunk));
   HandleScope hs(d);
+  const bool small = small_mode(d, B);
   const size_t frame = (size_t)src.Hs * src.Ws;
   for (int off = 0; off < B; off += kChunk) {
     const int nb = B - off < kChunk ? B - off : kChunk;
     RgbdSrc c = src;
     c.rgb = src.rgb + off * frame * 3;
     c.depth = src.depth + off * frame;
-    const int rc = forward_t<_Float16>(d, nullptr, nb, y + off * 2 * (size_t)d->n_kp, s, nullptr, &c,
-                                       px ? px + off * 2 * (size_t)d->n_kp : nullptr);
+    float* yc = y + off * 2 * (size_t)d->n_kp;
+    float* pc = px ? px + off * 2 * (size_t)d->n_kp : nullptr;
+    int rc;
+    if (fused) {
+      rc = forward_t<_Float16>(d, nullptr, nb, yc, s, nullptr, small, &c, pc);
+    } else {
+      rc = launch_preprocess(c.rgb, c.depth, nb, c.Hs, c.Ws, c.bgr, c.near_m, c.far_m, d->H, d->W, d->xin, s);
+      if (rc == PA_OK) rc = forward_chunk(d, d->xin, nb, yc, s, nullptr, small, pc);
+    }
     if (rc != PA_OK) return rc;
   }
   return PA_OK;
@@ -685,6 +739,7 @@ void pa_detector_destroy(pa_detector* d) {
   if (d->pool) hipFree(d->pool);
   if (d->cnt) hipFree(d->cnt);
   if (d->part) hipFree(d->part);
+  if (d->xin) hipFree(d->xin);
   delete d;
 }
 

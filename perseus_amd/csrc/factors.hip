@@ -785,6 +785,7 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
     Pose T[PPW];
     V3 pb[PPW];
     float2 yv[PPW];
+    bool off[PPW];  // a.nvalid: frame before its window's filled part
 #pragma unroll
     for (int h = 0; h < PPW; ++h) {
       const long ib = (u * PPW + h) * 64;
@@ -796,12 +797,21 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
       yv[h] = float2{yf[0], yf[1]};
       T[h] = load_pose(a.pose + f * 12);
       pb[h] = load3(a.corners + 3 * k);
+      const long t = f / a.L;
+      off[h] = a.nvalid ? (int)(f - t * a.L) < a.L - a.nvalid[t] : false;
     }
 #pragma unroll
     for (int h = 0; h < PPW; ++h) {
       const float px = kornia_denorm(yv[h].x, a.W);
       const float py = kornia_denorm(yv[h].y, a.H);
       proj_eval(T[h], pb[h], (double)px, (double)py, cam, r[h], J[h], e[h], stt[h]);
+      if (off[h]) {  // no measurement yet: status 2, zero residual / Jacobian / error
+        r[h][0] = r[h][1] = 0.0;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) J[h][c] = 0.0;
+        e[h] = 0.0;
+        stt[h] = 2;
+      }
     }
     if (ts) {
       asm volatile("" ::"v"(r[0][0]), "v"(r[PPW - 1][1]), "v"(J[PPW - 1][11]));  // compute done
@@ -893,11 +903,14 @@ __global__ __launch_bounds__(128, 2) void traj_all_kernel(pa_traj_args a, int mo
 // us for 3 x 24 against ~2.)  Then thread 0 predicts the new last frame with the
 // PoseDynamicsFactor model (factors.py:100-105): pose[L-1] = pose[L-2] Exp(dt [w; v_b]),
 // v_b = R^T v for a world-frame velocity; angvel / vel carried over.
+// nvalid (optional): frames of the window that hold a real measurement, + 1 per advance up
+// to L (pa_trajectory_linearize skips the projection factors of the others)
 constexpr int ADV_E = 4;
 __global__ __launch_bounds__(256) void window_advance_kernel(int L, int n_kp, const float* __restrict__ y_new,
                                                              float* y, double* pose, double* angvel, double* vel,
-                                                             double dt, int vel_frame) {
+                                                             double dt, int vel_frame, int32_t* nvalid) {
   const int t = blockIdx.x, e = threadIdx.x;
+  if (nvalid && e == 0) nvalid[t] = nvalid[t] < L ? nvalid[t] + 1 : L;
   const int ny = 2 * n_kp;
   float* yt = y + (size_t)t * L * ny;
   double* pt = pose + (size_t)t * L * 12;
@@ -1009,16 +1022,21 @@ __global__ __launch_bounds__(64) void window_retract_kernel(int T, int L, const 
 
 extern "C" {
 
-int pa_window_advance(int T, int L, int n_kp, const float* y_new, float* y, double* pose, double* angvel,
-                      double* vel, double dt, int vel_frame, void* stream) {
+int pa_window_advance_n(int T, int L, int n_kp, const float* y_new, float* y, double* pose, double* angvel,
+                        double* vel, int32_t* nvalid, double dt, int vel_frame, void* stream) {
   PA_CHECK(T >= 0 && L >= 1 && n_kp >= 1 && n_kp <= 32, "T=%d L=%d n_kp=%d", T, L, n_kp);
   if (T == 0) return PA_OK;
   PA_CHECK(y_new && y && pose && angvel && vel, "null pointer");
   PA_CHECK(vel_frame == PA_VEL_WORLD || vel_frame == PA_VEL_BODY, "vel_frame must be 'world' or 'body'.");
   hipLaunchKernelGGL(pa::window_advance_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, L, n_kp, y_new, y, pose,
-                     angvel, vel, dt, vel_frame);
+                     angvel, vel, dt, vel_frame, nvalid);
   PA_LAUNCH_CHECK();
   return PA_OK;
+}
+
+int pa_window_advance(int T, int L, int n_kp, const float* y_new, float* y, double* pose, double* angvel,
+                      double* vel, double dt, int vel_frame, void* stream) {
+  return pa_window_advance_n(T, L, n_kp, y_new, y, pose, angvel, vel, nullptr, dt, vel_frame, stream);
 }
 
 int pa_window_retract_newest(int T, int L, const double* delta, const int32_t* info, double* pose, double* angvel,

@@ -81,6 +81,7 @@ struct GnStage {
 };
 
 static __device__ int32_t gn_zero_i32[1];  // status source when no status array is given (zero-initialised)
+static __device__ double gn_zero_f64[2];   // projection source when K == 0 (the pointers may be null then)
 
 // Assembles frame f (of trajectory t, frame index l) with one wave: D_l, E_l (if l + 1 < L)
 // and g_l to the outputs a.D / a.E / a.g and to the LDS block `blk` (D | E | g).
@@ -112,17 +113,21 @@ __device__ __forceinline__ void gn_load_frame(const GnArgs& a, long f, GnFrameLo
   // (the status pointer test is uniform)
   const bool has_st = a.st_proj != nullptr;
   const int32_t* stp = has_st ? a.st_proj : gn_zero_i32;  // always a valid address
+  // K == 0: every projection load below is clamped to element 0 of a valid dummy (the
+  // caller may pass null projection arrays), and no lane uses the value
+  const double* jproj = K > 0 ? a.j_proj : gn_zero_f64;
+  const double* rproj = K > 0 ? a.r_proj : gn_zero_f64;
 #pragma unroll
   for (int q = 0; q < JR; ++q) {
     const int e = lane + 64 * q;
     const bool v = e < K * 12;
     const long u = fk + (v ? e / 12 : 0);
-    ld.jv[q] = a.j_proj[v ? fk * 12 + e : fk * 12];  // (u, c, row) = (e / 12, (e % 12) / 2, e & 1)
+    ld.jv[q] = jproj[v ? fk * 12 + e : (K > 0 ? fk * 12 : 0)];  // (u, c, row) = (e / 12, (e % 12) / 2, e & 1)
     ld.js[q] = stp[has_st ? u : 0];
   }
   const bool vr = lane < 2 * K;
   const long ur = fk + (vr ? lane >> 1 : 0);
-  ld.rv = a.r_proj[vr ? fk * 2 + lane : fk * 2];
+  ld.rv = rproj[vr ? fk * 2 + lane : (K > 0 ? fk * 2 : 0)];
   ld.rs = stp[has_st ? ur : 0];
   // pair factors: lane classes [0, 36) dynamics J (6 x 6 column-major; < 18 also the 6 x 3
   // J1 / J2), [36, 45) constant velocity (3 x 3), [45, 51) dynamics r, [51, 54) const-vel r
@@ -323,22 +328,25 @@ __device__ __forceinline__ void gn_build_frame(const GnArgs& a, long f, const Gn
       }
     }
   }
-  double* Dl = a.D + f * NB;
-  double* El = nxt ? a.E + ((long)t * npair + l) * NB : nullptr;
-  double* gl = a.g + f * NV;
+  // D / E / g go to the API outputs only when the caller asked for them (a.D null: the
+  // blocks stay in the solver's LDS ring; the streaming tick and GNPlan use delta only)
+  const bool out = a.D != nullptr;  // uniform
+  double* Dl = out ? a.D + f * NB : nullptr;
+  double* El = (out && nxt) ? a.E + ((long)t * npair + l) * NB : nullptr;
+  double* gl = out ? a.g + f * NV : nullptr;
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int i = lk + 4 * v;
     if (i >= NV) continue;
     if (li < NV) {
-      Dl[i * NV + li] = cD[v];
+      if (out) Dl[i * NV + li] = cD[v];
       blk[i * NV + li] = cD[v];
-      if (El) {
-        El[i * NV + li] = cE[v];
+      if (nxt) {
+        if (out) El[i * NV + li] = cE[v];
         blk[NB + i * NV + li] = cE[v];
       }
     } else if (li == NV) {
-      gl[i] = cD[v];
+      if (out) gl[i] = cD[v];
       blk[2 * NB + i] = cD[v];
     }
   }
@@ -1115,7 +1123,8 @@ int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const do
            pa::GN_KMAX);
   if (T == 0) return PA_OK;
   PA_CHECK(lambda >= 0.0, "gn: lambda %g < 0", lambda);
-  PA_CHECK(D && g && delta && ws && (L == 1 || E), "gn: null output / workspace pointer");
+  PA_CHECK(delta && ws, "gn: null delta / workspace pointer");
+  PA_CHECK((!D && !E && !g) || (D && g && (L == 1 || E)), "gn: D, E, g are given together (or all NULL)");
   PA_CHECK(n_kp == 0 || (r_proj && j_proj), "gn: null projection factors");
   PA_CHECK(L == 1 || (r_dyn && j_dyn0 && j_dyn1 && j_dyn2 && j_dyn3 && r_cv && j_cv0 && j_cv1),
            "gn: null dynamics / constant-velocity factors (Jacobians are required)");

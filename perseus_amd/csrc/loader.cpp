@@ -555,10 +555,14 @@ int pa_load_keypoint_items(const char* const* image_paths, const char* const* de
   };
   return guarded("pa_load_keypoint_items", [&]() {
     std::vector<std::thread> pool;
+    // reserved before any thread starts: emplace_back then never reallocates, so the only
+    // throw inside the loop is the thread's own construction (a bad_alloc here leaves no
+    // joinable thread behind)
+    pool.reserve(n_threads > 1 ? n_threads - 1 : 0);
     for (int t = 1; t < n_threads; ++t) {
       try {
         pool.emplace_back(work);
-      } catch (const std::system_error&) {
+      } catch (...) {
         break;  // fewer threads: the calling thread and those already started finish the batch
       }
     }

@@ -218,4 +218,18 @@ int launch_stem_pool_x3(const float* x, int B, int Cin, const _Float16* w, const
   return PA_OK;
 }
 
+// latency mode (a few frames): bands of 2 pooled rows, 32 workgroups per frame instead of 4
+// (stem.hip's short bands for the fp16 stem); the same arithmetic per pooled row
+int launch_stem_pool_x3_small(const float* x, int B, int Cin, const _Float16* w, const float* bias_s,
+                              const float* scale, _Float16* out, hipStream_t s) {
+  PA_CHECK(Cin >= 1 && Cin <= 4, "stem x3: Cin %d", Cin);
+  PA_CHECK((size_t)B * 64 * 64 * 128 * 2 < 0x7fffffffu, "stem x3: output over 2 GB");
+  if (B <= 0) return PA_OK;
+  constexpr int PBT = 2;
+  hipLaunchKernelGGL((stem_pool3_x3<PBT, 2>), dim3(64 / PBT, B), dim3(stemx3::NT), 0, s, x, B, Cin, w, bias_s, scale,
+                     out);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
 }  // namespace pa

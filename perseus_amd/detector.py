@@ -173,9 +173,10 @@ class KeypointCNN(nn.Module):
                            "set_variant")
 
     def set_split_k(self, max_batch: int) -> None:
-        """Latency mode (pa_detector_set_split_k): fp16 forwards of at most `max_batch`
-        frames run layers 2-4's stride-1 convs split-K (fills the chip at a few frames;
-        deterministic, not bit-identical to the batched kernels).  0 turns it off."""
+        """Latency mode (pa_detector_set_split_k): fp16 and fp16x3 forwards of at most
+        `max_batch` frames run short stem bands, small tiles and layers 2-4's convs split-K
+        (fills the chip at a few frames; deterministic, not bit-identical to the batched
+        kernels; fp16x3 keeps its 1e-3 px parity).  0 turns it off."""
         if not 0 <= max_batch <= 64:
             raise ValueError(f"split-K max batch {max_batch} not in [0, 64]")
         self._split_k = int(max_batch)
@@ -251,13 +252,13 @@ class KeypointCNN(nn.Module):
     def forward_rgbd(self, rgb: torch.Tensor, depth: torch.Tensor, bgr: bool = True, near: float | None = None,
                      far: float | None = None) -> torch.Tensor:
         """Camera frames -> keypoints (streaming.py:68-80 then :128): uint8 (B,Hs,Ws,3) + f32
-        metres (B,Hs,Ws) on the GPU, centre-cropped to 256x256.  fp16: the preprocess runs
-        inside the stem's row loads (pa_detector_forward_rgbd, no f32 input tensor); fp32: the
-        separate pa_preprocess_rgbd kernel, then forward().  Both give the bits of
-        forward(preprocess_rgbd(rgb, depth, ...))."""
+        metres (B,Hs,Ws) on the GPU, centre-cropped to 256x256, through pa_detector_forward_rgbd:
+        fp16: the preprocess runs inside the stem's row loads (no f32 input tensor); fp16x3 /
+        fp32: the preprocess kernel into the handle's staging, then the forward.  All give the
+        bits of forward(preprocess_rgbd(rgb, depth, ...))."""
         if rgb.device.type != "cuda" or depth.device.type != "cuda":
             raise RuntimeError("forward_rgbd expects device tensors")
-        if self.precision != "fp16" or self.num_channels != 4:
+        if self.num_channels != 4:
             return self.forward(preprocess_rgbd(rgb, depth, self.H, self.W, bgr=bgr, near=near, far=far))
         rgb = rgb.contiguous()
         depth = depth.contiguous().float()
@@ -268,7 +269,7 @@ class KeypointCNN(nn.Module):
         dev = rgb.device
         h = self._ensure_handle(dev)
         L = _lib.lib()
-        _lib.check(L.pa_detector_set_precision(h, _lib.PREC_FP16), "set_precision")
+        _lib.check(L.pa_detector_set_precision(h, _lib.precision_code(self.precision)), "set_precision")
         y = torch.empty((B, 2 * self.n_keypoints), dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
             _lib.check(L.pa_detector_forward_rgbd(h, rgb.data_ptr(), depth.data_ptr(), B, Hs, Ws, int(bgr),

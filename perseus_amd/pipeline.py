@@ -52,11 +52,14 @@ def _isig(sigmas, dim, dev):
 
 def prepare_trajectories(y: torch.Tensor, poses, vels, angvels, corners, K, *, T: int, L: int, dt: float,
                          vel_frame: str = "world", camera_pose=None, H: int = 256, W: int = 256,
-                         proj_sigmas=None, dyn_sigmas=None, cv_sigmas=None, jacobians: bool = True):
+                         proj_sigmas=None, dyn_sigmas=None, cv_sigmas=None, jacobians: bool = True,
+                         nvalid: torch.Tensor | None = None):
     """Stage inputs on the device and allocate outputs: returns (args, out).  `args`
     (a pa_traj_args) can be launched repeatedly with `launch(args, device)`; `out`
     holds the output tensors (Jacobians as (n, cols, rows) column-major buffers) and
-    keeps every staged input alive."""
+    keeps every staged input alive.  nvalid (optional, int32 (T,) on the device, read at
+    every launch): frames with a measurement, counted from the window's end; the projection
+    factors of the others get status 2 and zero residual / Jacobian (the GN step skips them)."""
     if y.device.type != "cuda":
         raise RuntimeError("linearize_trajectories expects the detector output on the GPU (no CPU fallback)")
     if vel_frame not in ("world", "body"):
@@ -92,9 +95,13 @@ def prepare_trajectories(y: torch.Tensor, poses, vels, angvels, corners, K, *, T
     a.dt = float(dt)
     a.vel_frame = _lib.VEL_WORLD if vel_frame == "world" else _lib.VEL_BODY
     a.isig_proj, a.isig_dyn, a.isig_cv = _lib.ptr(isp), _lib.ptr(isd), _lib.ptr(isc)
+    if nvalid is not None and (nvalid.device != dev or nvalid.dtype != torch.int32 or nvalid.numel() != T
+                               or not nvalid.is_contiguous()):
+        raise RuntimeError(f"nvalid must be a contiguous int32 ({T},) tensor on {dev}")
+    a.nvalid = _lib.ptr(nvalid)
     for k in ("r_proj", "err_proj", "status", "r_dyn", "err_dyn", "r_cv", "err_cv", *_JAC):
         setattr(a, k, _lib.ptr(out[k]))
-    out["_keep"] = (y, P, V, Wv, Cn, Kt, Tc, isp, isd, isc)  # inputs stay alive until the stream drains
+    out["_keep"] = (y, P, V, Wv, Cn, Kt, Tc, isp, isd, isc, nvalid)  # inputs stay alive until the stream drains
     return a, out
 
 
@@ -137,11 +144,12 @@ class GNPlan:
     pa_trajectory_gn_step) over `lin` = the outputs of prepare_trajectories /
     linearize_trajectories run with whitening sigmas and Jacobians, with every output and
     the workspace allocated once, so `launch` can be captured in a HIP graph and replayed
-    (the streaming pose stage).  out: D (T*L,12,12), E (T*(L-1),12,12), g (T*L,12),
-    delta (T*L,12), info (T,) int32 (0 = solved).  Variable block per frame:
-    [pose (6) | angvel (3) | vel (3)]."""
+    (the streaming pose stage).  out: delta (T*L,12), info (T,) int32 (0 = solved), and
+    with blocks=True also the normal-matrix blocks D (T*L,12,12), E (T*(L-1),12,12) and
+    g (T*L,12) (blocks=False: they stay on chip, the launch writes delta and info only).
+    Variable block per frame: [pose (6) | angvel (3) | vel (3)]."""
 
-    def __init__(self, lin: dict, *, T: int, L: int, lam: float = 0.0):
+    def __init__(self, lin: dict, *, T: int, L: int, lam: float = 0.0, blocks: bool = False):
         if lin.get("j_proj") is None:
             raise RuntimeError("gn_step needs the Jacobians (linearize with jacobians=True)")
         dev = lin["r_proj"].device
@@ -153,8 +161,9 @@ class GNPlan:
         def e(*shape, dtype=torch.float64):
             return torch.empty(shape, dtype=dtype, device=dev)
 
-        self.out = {"D": e(T * L, 12, 12), "E": e(max(m, 1), 12, 12), "g": e(T * L, 12), "delta": e(T * L, 12),
-                    "info": e(T, dtype=torch.int32)}
+        self.out = {"delta": e(T * L, 12), "info": e(T, dtype=torch.int32)}
+        if blocks:
+            self.out.update(D=e(T * L, 12, 12), E=e(max(m, 1), 12, 12), g=e(T * L, 12))
         L_ = _lib.lib()
         self.ws = torch.empty(max(int(L_.pa_trajectory_gn_workspace(T, L)), 8), dtype=torch.uint8, device=dev)
         self.dev = dev
@@ -166,7 +175,8 @@ class GNPlan:
             _lib.check(_lib.lib().pa_trajectory_gn_step(
                 self.T, self.L, self.n_kp, p(lin["r_proj"]), p(lin["j_proj"]), p(lin.get("status")), p(lin["r_dyn"]),
                 p(lin["j_dyn0"]), p(lin["j_dyn1"]), p(lin["j_dyn2"]), p(lin["j_dyn3"]), p(lin["r_cv"]),
-                p(lin["j_cv0"]), p(lin["j_cv1"]), self.lam, p(out["D"]), p(out["E"]), p(out["g"]), p(out["delta"]),
+                p(lin["j_cv0"]), p(lin["j_cv1"]), self.lam, p(out.get("D")), p(out.get("E")), p(out.get("g")),
+                p(out["delta"]),
                 p(out["info"]), p(self.ws), self.ws.numel(), _lib.stream_of(self.dev)), "pa_trajectory_gn_step")
 
 
@@ -175,7 +185,7 @@ def gn_step(lin: dict, *, T: int, L: int, lam: float = 0.0) -> dict:
     pa_trajectory_gn_step) from `linearize_trajectories(...)` run with whitening sigmas and
     Jacobians.  Returns D (T*L,12,12), E (T*(L-1),12,12), g (T*L,12), delta (T*L,12) and
     info (T,) int32 (0 = solved).  Variable block per frame: [pose (6) | angvel (3) | vel (3)]."""
-    plan = GNPlan(lin, T=T, L=L, lam=lam)
+    plan = GNPlan(lin, T=T, L=L, lam=lam, blocks=True)
     plan.launch()
     out = dict(plan.out)
     out["E"] = out["E"][:plan.m]
@@ -183,18 +193,20 @@ def gn_step(lin: dict, *, T: int, L: int, lam: float = 0.0) -> dict:
     return out
 
 
-def window_advance(y_new: torch.Tensor, win: dict, *, dt: float, vel_frame: str = "world") -> None:
+def window_advance(y_new: torch.Tensor, win: dict, *, dt: float, vel_frame: str = "world",
+                   nvalid: torch.Tensor | None = None) -> None:
     """pa_window_advance on the device's current stream: every trajectory's window
     (win: y (T, L, 2K) f32, pose (T, L, 12), angvel / vel (T, L, 3) f64) moves one frame,
     y_new (T, 2K) becomes its last frame, whose pose is predicted by the
-    PoseDynamicsFactor model (factors.py:100-105)."""
+    PoseDynamicsFactor model (factors.py:100-105).  nvalid (optional, int32 (T,)): the
+    window's count of real frames, += 1 up to L (pa_window_advance_n)."""
     T, L, ny = win["y"].shape
     dev = win["y"].device
     with torch.cuda.device(dev):
-        _lib.check(_lib.lib().pa_window_advance(
+        _lib.check(_lib.lib().pa_window_advance_n(
             T, L, ny // 2, y_new.data_ptr(), win["y"].data_ptr(), win["pose"].data_ptr(), win["angvel"].data_ptr(),
-            win["vel"].data_ptr(), float(dt), _lib.VEL_WORLD if vel_frame == "world" else _lib.VEL_BODY,
-            _lib.stream_of(dev)), "pa_window_advance")
+            win["vel"].data_ptr(), _lib.ptr(nvalid), float(dt),
+            _lib.VEL_WORLD if vel_frame == "world" else _lib.VEL_BODY, _lib.stream_of(dev)), "pa_window_advance")
 
 
 def window_retract(win: dict, delta: torch.Tensor, info: torch.Tensor | None = None,

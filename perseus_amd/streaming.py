@@ -13,13 +13,16 @@ Gauss-Newton step per tick.  Per tick:
 
   host: frames -> pinned staging (centre crop rows only, or the full frame)
   GPU (one hipGraph replay on a private stream): H2D -> pa_detector_forward_rgbd_px
-       (B = n_cams; the preprocess runs inside the stem's row loads, the denormalize in the
-       head; fp32: pa_preprocess_rgbd + pa_detector_forward + pa_keypoints_postprocess)
-       [pose stage] -> pa_window_advance (window shifts one frame, the new keypoints
-       appended, the new pose predicted by the dynamics model) -> pa_trajectory_linearize
-       (whitened factors of every camera's window) -> pa_trajectory_gn_step ->
-       pa_window_retract_newest (pose Exp(delta), velocities += delta, newest poses out)
-       -> ONE D2H of [pixels | info | newest poses] (and one H2D of [rgb | depth] at the start)
+       (B = n_cams; fp16: the preprocess runs inside the stem's row loads; fp16x3 / fp32: the
+       preprocess kernel, then the forward; the denormalize in the head), in the small-batch
+       latency mode for fp16 and fp16x3 (the parity-grade tick)
+       [pose stage] -> pa_window_advance_n (window shifts one frame, the new keypoints
+       appended, the new pose predicted by the dynamics model, the count of real frames + 1)
+       -> pa_trajectory_linearize (whitened factors of every camera's window; frames not yet
+       filled by a real tick carry no projection factors) -> pa_trajectory_gn_step (delta and
+       info only) -> pa_window_retract_newest (pose Exp(delta), velocities += delta, newest
+       poses out) -> ONE D2H of [pixels | info | newest poses] (and one H2D of [rgb | depth]
+       at the start)
   host: wait for the replay, return (n_cams, K, 2) pixel coordinates (and the poses).
 
 The graph removes the per-launch CPU cost of the ~26 launches (the forward at B=3
@@ -89,8 +92,9 @@ class StreamingPipeline:
 
         self.rgb_h, self.depth_h, self.px_h, self.info_h, self.pose_h = views(self.in_h, self.out_h)
         self.rgb_d, self.depth_d, self.px_d, self.info_d, self.pose_d = views(self.in_d, self.out_d)
-        self.x = torch.empty((n, 4, self.H, self.W), dtype=torch.float32, device=self.dev)
         self.y = torch.empty((n, 2 * K), dtype=torch.float32, device=self.dev)
+        self.y_h = torch.empty((n, 2 * K), dtype=torch.float32).pin_memory()  # tick_keypoints' input
+        self.pose_graph = None
         self.stream = torch.cuda.Stream(self.dev)
         # A private handle: the captured graph holds its weight and workspace pointers, so
         # nothing the model does later (a larger batch growing its workspace, a weight
@@ -101,8 +105,9 @@ class StreamingPipeline:
         _lib.check(L.pa_detector_set_precision(self._h, _lib.precision_code(model.precision)), "set_precision")
         _lib.check(L.pa_detector_reserve(self._h, n), "reserve")
         # latency mode: a batch of n_cams frames leaves most CUs idle in the batched kernels
-        # (pa_detector_set_split_k; same results as model.set_split_k(n_cams) + forward)
-        self.split_k = bool(split_k) and n <= 64
+        # (pa_detector_set_split_k; same results as model.set_split_k(n_cams) + forward;
+        # fp16 and fp16x3, fp32 has no such mode)
+        self.split_k = bool(split_k) and n <= 64 and model.precision != "fp32"
         _lib.check(L.pa_detector_set_split_k(self._h, n if self.split_k else 0), "set_split_k")
         if model.num_channels != 4:
             raise ValueError("StreamingPipeline feeds RGBD (num_channels=4)")
@@ -123,27 +128,25 @@ class StreamingPipeline:
             self.graph = g
 
     def _enqueue(self):
-        """H2D, preprocess, forward, postprocess, [pose stage], D2H on the current stream."""
+        """H2D, preprocess + forward + denormalize, [pose stage], D2H on the current stream."""
         L = _lib.lib()
         s = torch.cuda.current_stream(self.dev).cuda_stream
         self.in_d.copy_(self.in_h, non_blocking=True)
-        if self.model.precision != "fp16":  # fp32 / fp16x3: preprocess kernel, then the forward
-            _lib.check(L.pa_preprocess_rgbd(self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n, self.sh, self.sw,
-                                            int(self.bgr), self.near, self.far, self.H, self.W, self.x.data_ptr(), s),
-                       "preprocess")
-            _lib.check(L.pa_detector_forward(self._h, self.x.data_ptr(), self.n, self.y.data_ptr(), s), "forward")
-            _lib.check(L.pa_keypoints_postprocess(self.y.data_ptr(), None, self.n, self.model.n_keypoints, self.H,
-                                                  self.W, self.px_d.data_ptr(), None, s), "postprocess")
-        else:  # fp16: the preprocess runs inside the stem's row loads (SURVEY 8f.1), the denormalize in the head
-            _lib.check(L.pa_detector_forward_rgbd_px(self._h, self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n,
-                                                     self.sh, self.sw, int(self.bgr), self.near, self.far,
-                                                     self.y.data_ptr(), self.px_d.data_ptr(), s), "forward_rgbd_px")
-        if self.pose_L:  # the pose stage, all on this stream (HBM-resident window)
-            pipeline.window_advance(self.y, self.win, dt=self.dt, vel_frame=self.vel_frame)
-            pipeline.launch(self.traj_args, self.dev)
-            self.gn.launch()  # info straight into the output block
-            pipeline.window_retract(self.win, self.gn.out["delta"], self.gn.out["info"], newest=self.pose_d)
+        # fp16: the preprocess runs inside the stem's row loads (SURVEY 8f.1); fp16x3 / fp32: the
+        # preprocess kernel into the handle's staging, then the forward; the denormalize in the head
+        _lib.check(L.pa_detector_forward_rgbd_px(self._h, self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n,
+                                                 self.sh, self.sw, int(self.bgr), self.near, self.far,
+                                                 self.y.data_ptr(), self.px_d.data_ptr(), s), "forward_rgbd_px")
+        if self.pose_L:
+            self._enqueue_pose()
         self.out_h.copy_(self.out_d, non_blocking=True)  # pixels (+ info, newest poses): one D2H
+
+    def _enqueue_pose(self):
+        """The pose stage on the current stream, from the keypoints in self.y (HBM-resident window)."""
+        pipeline.window_advance(self.y, self.win, dt=self.dt, vel_frame=self.vel_frame, nvalid=self.nvalid)
+        pipeline.launch(self.traj_args, self.dev)
+        self.gn.launch()  # delta, and info straight into the output block
+        pipeline.window_retract(self.win, self.gn.out["delta"], self.gn.out["info"], newest=self.pose_d)
 
     def _init_pose_stage(self, K, corners, dt, vel_frame, proj_sigma, dyn_sigma, cv_sigma, lam, init_pose, init_vel,
                          init_angvel):
@@ -165,19 +168,25 @@ class StreamingPipeline:
         self.win = {"y": torch.zeros((n, Lw, 2 * nk), dtype=torch.float32, device=dev),
                     "pose": torch.empty((n, Lw, 12), **f64), "angvel": torch.empty((n, Lw, 3), **f64),
                     "vel": torch.empty((n, Lw, 3), **f64)}
+        # real frames per camera window (from its end): until L ticks have run, the frames
+        # before them are the initial state with no measurement, and carry no projection factor
+        self.nvalid = torch.zeros(n, dtype=torch.int32, device=dev)
         self.traj_args, self.lin = pipeline.prepare_trajectories(
             self.win["y"].view(n * Lw, 2 * nk), self.win["pose"].view(n * Lw, 12), self.win["vel"].view(n * Lw, 3),
             self.win["angvel"].view(n * Lw, 3), corners, K, T=n, L=Lw, dt=self.dt, vel_frame=vel_frame, H=self.H,
-            W=self.W, proj_sigmas=[proj_sigma] * 2, dyn_sigmas=[dyn_sigma] * 6, cv_sigmas=[cv_sigma] * 3)
+            W=self.W, proj_sigmas=[proj_sigma] * 2, dyn_sigmas=[dyn_sigma] * 6, cv_sigmas=[cv_sigma] * 3,
+            nvalid=self.nvalid)
         for k in ("y", "pose", "vel", "angvel"):  # linearize reads the window in place, no staging copy
             assert self.lin["_keep"][("y", "pose", "vel", "angvel").index(k)].data_ptr() == self.win[k].data_ptr()
         self.gn = pipeline.GNPlan(self.lin, T=n, L=Lw, lam=lam)
         self.gn.out["info"] = self.info_d  # the GN step writes info into the output block
 
     def reset_window(self) -> None:
-        """Every frame of every camera's window back to the initial state (keypoints 0)."""
+        """Every frame of every camera's window back to the initial state (keypoints 0, no
+        real frame: the next tick's window holds one measured frame)."""
         with torch.cuda.stream(self.stream):
             self.win["y"].zero_()
+            self.nvalid.zero_()
             for k in ("pose", "vel", "angvel"):
                 self.win[k].copy_(torch.as_tensor(self._init[k], device=self.dev)[:, None, :]
                                   .expand_as(self.win[k]))
@@ -222,9 +231,37 @@ class StreamingPipeline:
         px = self(rgb, depth)
         return px, self.pose_h.numpy().copy(), self.info_h.numpy().copy()
 
+    def tick_keypoints(self, y) -> tuple:
+        """The pose stage alone on given normalized keypoints y (n, 2K) (the detector's output
+        convention, validate.py:139-141): the same launches as a tick's pose stage, from
+        self.y, captured as their own graph when graph=True.  Returns (newest pose (n, 12),
+        GN info (n,)).  For driving the smoother with known measurements."""
+        if not self.pose_L:
+            raise RuntimeError("tick_keypoints() needs the pose stage (pose_window > 0)")
+        self.y_h.numpy()[:] = np.asarray(y, np.float32).reshape(self.y_h.shape)
+
+        def enqueue():
+            self.y.copy_(self.y_h, non_blocking=True)
+            self._enqueue_pose()
+            self.out_h.copy_(self.out_d, non_blocking=True)
+
+        with torch.cuda.stream(self.stream):
+            if self.graph is not None:
+                if self.pose_graph is None:  # captured on first use (every buffer exists already)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=self.stream):
+                        enqueue()
+                    self.pose_graph = g
+                self.pose_graph.replay()
+            else:
+                enqueue()
+        self.stream.synchronize()
+        return self.pose_h.numpy().copy(), self.info_h.numpy().copy()
+
     def close(self) -> None:
-        """Drop the graph, then the handle it captured."""
+        """Drop the graphs, then the handle they captured."""
         self.graph = None
+        self.pose_graph = None
         if getattr(self, "_h", None) is not None:
             torch.cuda.synchronize(self.dev)
             _lib.lib().pa_detector_destroy(self._h)

@@ -195,6 +195,48 @@ def test_split_k_latency_mode():
     assert torch.equal(m(x[:3]), y_batched[:3])
 
 
+def test_split_k_latency_mode_fp16x3():
+    """The parity-grade latency mode (fp16x3 + pa_detector_set_split_k, conv_splitk.hip X3
+    forms): short stem bands, layer1 / layer2 entry on small tiles, every other conv of
+    layers 2-4 split-K + splitk_reduce_x3.  Within the 1e-3 px parity bar of the golden
+    reference outputs and of the f64 oracle, deterministic, batch-invariant among
+    latency-mode batches; larger batches keep the batched X3 kernels' bits."""
+    xs = synth.synthetic_frames(7, 9, first=3)
+    x = torch.from_numpy(xs).cuda()
+    m = model(0, precision="fp16x3")
+    y_batched = m(x)
+    m.set_split_k(8)
+    names = [n for n, _ in m.profile(x[:3])[0]]
+    # split: layer2's 3 stride-1 convs, layer3 / layer4 entry + 3 convs each (each conv + its reduce: one name)
+    assert sum(n.endswith("_splitk") for n in names) == 11, names
+    assert sum(n.endswith("_small") for n in names) == 6, names  # stem, layer1's 4 convs, layer2's entry
+    y8 = m(x[:8])
+    assert torch.equal(y8, m(x[:8]))
+    for B in (1, 3, 5):
+        assert torch.equal(m(x[:B]), y8[:B]), B
+    assert torch.equal(m(x), y_batched)  # B = 9 > 8: batched kernels
+    y64 = R.run(synth.synthetic_state_dict(0), xs[:8], torch.float64)
+    err64 = np.abs(y8.cpu().numpy() - y64).max() * PX
+    errb = np.abs(y8.cpu().numpy() - y_batched[:8].cpu().numpy()).max() * PX
+    print(f"fp16x3 split-K B<=8: max px err vs f64 {err64:.3e}; vs batched X3 kernels {errb:.3e} px")
+    assert err64 <= FP32_PX_MAX and errb <= FP32_PX_MAX
+    m.set_split_k(0)
+    assert torch.equal(m(x[:3]), y_batched[:3])
+
+
+@pytest.mark.parametrize("idx", range(4))
+def test_fp16x3_latency_mode_matches_reference_golden(gold, idx):
+    """The golden cases (the reference's own CPU outputs) through the fp16x3 latency mode."""
+    name, seed, x = cases()[idx]
+    m = model(seed, precision="fp16x3")
+    m.set_split_k(x.shape[0])
+    y = m(torch.from_numpy(x).cuda()).cpu().numpy()
+    err_ref = np.abs(y - gold[f"{name}/y_ref_f32"]).max() * PX
+    err64 = np.abs(y - gold[f"{name}/y_oracle_f64"]).max() * PX
+    print(f"{name}: fp16x3 latency mode max px err vs ref {err_ref:.3e} vs f64 {err64:.3e}")
+    assert err_ref <= FP32_PX_MAX and err64 <= FP32_PX_MAX
+
+
 def test_cpu_input_like_streaming_py():
     """streaming.py:126-128 calls the model on a CPU tensor: result comes back on CPU."""
     x = synth.synthetic_frames(0, 1)

@@ -101,3 +101,37 @@ def test_camera_counts_latency_mode_vs_batched_and_oracle(model, n):
     y64 = R.run(synth.synthetic_state_dict(0), x.cpu().numpy(), torch.float64)
     px64 = R.denormalize_f32(y64.astype(np.float32)).reshape(n, -1, 2)
     assert np.sqrt(((out - px64) ** 2).sum(-1)).max() <= 0.1  # px-L2, the fp16 budget (test_detector_gpu.FP16_PX_MAX)
+
+
+@pytest.fixture(scope="module")
+def model_x3():
+    m = KeypointCNN(num_channels=4, precision="fp16x3")
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
+    return m
+
+
+@pytest.mark.parametrize("n", [1, 3, 5])
+def test_parity_grade_tick_fp16x3(model_x3, n):
+    """The parity-grade streaming tick (fp16x3 in its latency mode): graph replay == eager bit
+    for bit, the pixels are model.set_split_k(n) + forward's on the preprocessed frames, and
+    every keypoint coordinate is within 1e-3 px of the f64 oracle's (north_star) on the same
+    frames (streaming.py:68-80 arithmetic)."""
+    rgb, d = _frames(21 + n, n)
+    g = StreamingPipeline(model_x3, n_cams=n, graph=True)
+    e = StreamingPipeline(model_x3, n_cams=n, graph=False)
+    out = g(rgb, d)
+    np.testing.assert_array_equal(out, e(rgb, d))
+    g.close()
+    e.close()
+    x = preprocess_rgbd(torch.as_tensor(rgb).cuda(), torch.as_tensor(d).cuda())
+    model_x3.set_split_k(n)
+    try:
+        y = model_x3(x)
+    finally:
+        model_x3.set_split_k(0)
+    np.testing.assert_array_equal(out, R.denormalize_f32(y.cpu().numpy()).reshape(n, -1, 2))
+    y64 = R.run(synth.synthetic_state_dict(0), x.cpu().numpy(), torch.float64)
+    px64 = ((y64 + 1.0) * 127.5).reshape(n, -1, 2)  # exact denormalize of the f64 outputs
+    err = np.abs(out.astype(np.float64) - px64).max()
+    print(f"fp16x3 tick, {n} camera(s): max |px - px_f64| = {err:.3e}")
+    assert err <= 1e-3
