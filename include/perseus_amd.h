@@ -229,8 +229,9 @@ int pa_trajectory_gn_step(int T, int L, int n_kp, const double* r_proj, const do
  * angvel and vel (T*L, 3), all device, frame f = t*L + l.
  * pa_window_advance: shifts every array one frame towards l = 0 (frame 0 dropped),
  * writes y_new[t] (T, 2K) as frame L-1 and predicts pose[L-1] = pose[L-2] Exp(dt [w; v_b])
- * (the PoseDynamicsFactor model, factors.py:100-105; v_b = R^T v for PA_VEL_WORLD) with
- * angvel / vel carried over from frame L-2.
+ * (the PoseDynamicsFactor model, factors.py:100-105; v_b = R^T v for PA_VEL_WORLD), v = vel
+ * of frame L-2 carried over and w = the angular velocity frame L-2 held before the shift
+ * (the newest one a factor constrains; L >= 3), which frames L-2 and L-1 both take.
  * pa_window_retract: pose <- pose Exp(delta[0:6]) (Pose3 retract, Expmap chart),
  * angvel += delta[6:9], vel += delta[9:12] for pa_trajectory_gn_step's delta (T*L, 12);
  * trajectories with info[t] != 0 are left unchanged (info may be NULL). */

@@ -423,7 +423,11 @@ def projection_batch(Tb, p_b, z, K, Tc=None):
 def window_advance(win: dict, y_new, dt, vel_frame="world") -> dict:
     """win: y (T, L, 2K), pose (T, L, 12), angvel / vel (T, L, 3); returns the advanced
     copy: frames shift one towards l = 0, y_new (T, 2K) appended, the new pose =
-    pose[L-2] Exp(dt [w; v_b]) with v_b = R^T v (world) or v (body), velocities carried."""
+    pose[L-2] Exp(dt [w; v_b]) with v_b = R^T v (world) or v (body), v = vel[L-2] carried.
+    w is the angular velocity of the window's second-to-last frame BEFORE the shift (the
+    newest one a PoseDynamicsFactor constrains: the last frame's angular velocity enters no
+    factor, so its value holds no information) and becomes the angular velocity of both
+    new last frames (L >= 3; L = 2 carries frame 1's)."""
     out = {k: np.array(v, copy=True) for k, v in win.items()}
     for k in out:
         out[k][:, :-1] = win[k][:, 1:]
@@ -431,10 +435,11 @@ def window_advance(win: dict, y_new, dt, vel_frame="world") -> dict:
     T, L = out["pose"].shape[:2]
     for t in range(T):
         T1 = unpack(out["pose"][t, L - 2])
-        w = out["angvel"][t, L - 2]
+        w = np.array(win["angvel"][t, L - 2] if L >= 3 else out["angvel"][t, L - 2], copy=True)
         v = out["vel"][t, L - 2]
         vb = T1[0].T @ v if vel_frame == "world" else v
         out["pose"][t, L - 1] = pack(compose(T1, pose_exp(np.concatenate([dt * w, dt * vb]))))
+        out["angvel"][t, L - 2] = w
         out["angvel"][t, L - 1] = w
         out["vel"][t, L - 1] = v
     return out

@@ -81,6 +81,8 @@ int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname);
 
 // fp16, LDS-DMA deep ring (conv_s2x.h, conv_s2x_l.hip), layers 2-4
 int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
+// fp16, 8 x 16 x 128 tiles with the row-split patch (conv_s2w.h), layers 2-3 (shipped there)
+int launch_conv3x3s2_w(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
 
 template <typename T>
 int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);

@@ -312,10 +312,13 @@ template <typename T>
 int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
   if constexpr (std::is_same<T, _Float16>::value) {
-    // conv_s2x (shipped; g_variant[6] = 10..39 its alternatives 0..29); 3: the one-tile
-    // kernel below (bit-identical reference for the variant test)
-    if (g_variant[6] == 0 || (g_variant[6] >= 10 && g_variant[6] <= 39))
-      return launch_conv3x3s2_x(a, g_variant[6] == 0 ? 0 : g_variant[6] - 10, s, kname);
+    // shipped: conv_s2w (layers 2 / 3; g_variant[6] = 40..47 its alternatives 0..7) and
+    // conv_s2x (layer4; g_variant[6] = 10..39 its alternatives 0..29 on every layer); 3: the
+    // one-tile kernel below (bit-identical reference of conv_s2x for the variant test)
+    const int v = g_variant[6];
+    const bool w = v == 0 || (v >= 40 && v <= 47);
+    if (w && a.Hout != 8) return launch_conv3x3s2_w(a, v == 0 ? 0 : v - 40, s, kname);
+    if (w || (v >= 10 && v <= 39)) return launch_conv3x3s2_x(a, v >= 10 && v <= 39 ? v - 10 : 0, s, kname);
   }
   if (a.Hout == 32) {
     if (kname) *kname = "conv3x3s2ds_l2";

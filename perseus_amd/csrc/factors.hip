@@ -902,7 +902,12 @@ __global__ __launch_bounds__(128, 2) void traj_all_kernel(pa_traj_args a, int mo
 // reads.  (Round 2's per-element loop waited out one load-store round trip per frame: 18.7
 // us for 3 x 24 against ~2.)  Then thread 0 predicts the new last frame with the
 // PoseDynamicsFactor model (factors.py:100-105): pose[L-1] = pose[L-2] Exp(dt [w; v_b]),
-// v_b = R^T v for a world-frame velocity; angvel / vel carried over.
+// v_b = R^T v for a world-frame velocity, v = vel[L-2] carried over; w = the angular
+// velocity frame L-2 had before the shift (L >= 3), which both new last frames take.  The
+// last frame's angular velocity enters no factor (ConstantVelocityFactor constrains the
+// linear velocity only, factors.py:145-171), so the GN step never corrects it: carried
+// from frame L-1 instead, it kept its initial value forever and every prediction used it
+// (a 40-tick tracking test plateaued at 3e-4 rad; with this, 2e-7).
 // nvalid (optional): frames of the window that hold a real measurement, + 1 per advance up
 // to L (pa_trajectory_linearize skips the projection factors of the others)
 constexpr int ADV_E = 4;
@@ -911,6 +916,11 @@ __global__ __launch_bounds__(256) void window_advance_kernel(int L, int n_kp, co
                                                              double dt, int vel_frame, int32_t* nvalid) {
   const int t = blockIdx.x, e = threadIdx.x;
   if (nvalid && e == 0) nvalid[t] = nvalid[t] < L ? nvalid[t] + 1 : L;
+  // the angular velocity of frame L-2 BEFORE the shift: the newest one a dynamics factor
+  // constrains (frame L-1's enters no factor, so its value holds no information); read
+  // before the first barrier, i.e. before any shifted store
+  V3 wc{0.0, 0.0, 0.0};
+  if (e == 0 && L >= 3) wc = load3(angvel + ((size_t)t * L + L - 2) * 3);
   const int ny = 2 * n_kp;
   float* yt = y + (size_t)t * L * ny;
   double* pt = pose + (size_t)t * L * 12;
@@ -958,7 +968,12 @@ __global__ __launch_bounds__(256) void window_advance_kernel(int L, int n_kp, co
   __syncthreads();
   if (e == 0 && L >= 2) {
     const Pose T1 = load_pose(pt + (L - 2) * 12);
-    const V3 w = load3(wt + (L - 2) * 3), v = load3(vt + (L - 2) * 3);
+    const V3 w = L >= 3 ? wc : load3(wt + (L - 2) * 3), v = load3(vt + (L - 2) * 3);
+    if (L >= 3) {  // the shifted frame L-2 takes it too
+      wt[(L - 2) * 3 + 0] = w.x;
+      wt[(L - 2) * 3 + 1] = w.y;
+      wt[(L - 2) * 3 + 2] = w.z;
+    }
     const V3 vb = vel_frame == PA_VEL_WORLD ? mtv(T1.R, v) : v;
     const V3 xw = dt * w, xv = dt * vb;
     const Pose P = compose(T1, pose_exp(xw, xv, ang(xw)));

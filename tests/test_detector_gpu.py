@@ -353,27 +353,40 @@ def test_kernel_variants_agree_bit_for_bit(B):
     """The persistent kernels (layer1 weight-resident conv, stride-2 + downsample)
     and the one-tile-per-workgroup kernels they replace accumulate in the same order:
     identical outputs, at batches below and above one tile per CU.  (Stem variants 10
-    and 16 are version 3 of the stem at two band heights.)"""
+    and 16 are version 3 of the stem at two band heights.)  The shipped layer2 / layer3
+    stride-2 entries (conv_s2w.h, row-split patch) sum the conv's taps in another order
+    (kh = 1, 0, 2) than conv_s2x.h and the one-tile kernel (kh = 0, 1, 2): they agree bit for
+    bit with their own variants, and the conv_s2x.h forms (variant 6:10 = conv_s2x.h on
+    every entry) with each other; the two orders stay within 0.05 px."""
     m = model(0)
     x = torch.from_numpy(synth.synthetic_frames(2, B)).cuda()
-    y0 = m(x)
-    sets = (
-        ((1, 3), (2, 1), (3, 1), (4, 1), (6, 3), (0, 10)),
-        ((1, 30), (7, 1)),  # layer1: register-staged kernel on every conv; the generic head
-        ((1, 32),),  # layer1: the one-tile patch kernel (independent of the shipped LDS-DMA kernel)
-        ((7, 3),),  # avgpool + fc fused into layer4's last conv instead of head_fp16
-        ((6, 11),),  # stride-2 entries: one tile per workgroup (layer2: the round-2a 8x16 kernel)
-        ((6, 26),),  # multi-tile workgroups: layer2 4 waves of 32x64; layer3 as shipped
-        ((6, 27),),  # layer2 prefetch distance 3; layer3 two 4x16 tiles per workgroup
-        ((0, 16),),  # stem: version 3 (every wave convolves and moves rows) vs the shipped role split
-    )
-    for vs in sets:
+
+    def run(vs):
         try:
             m.set_variants(dict(vs))
-            y1 = m(x)
+            return m(x)
         finally:
             m.set_variants({})
-        assert torch.equal(y0, y1), vs
+
+    y0 = m(x)
+    ys2x = run({6: 10})
+    assert (y0 - ys2x).abs().max().item() * PX <= 0.05
+    sets = (
+        (((1, 3), (2, 1), (3, 1), (4, 1), (0, 10)), y0),
+        (((1, 30), (7, 1)), y0),  # layer1: register-staged kernel on every conv; the generic head
+        (((1, 32),), y0),  # layer1: the one-tile patch kernel (independent of the shipped LDS-DMA kernel)
+        (((7, 3),), y0),  # avgpool + fc fused into layer4's last conv instead of head_fp16
+        (((0, 16),), y0),  # stem: version 3 (every wave convolves and moves rows) vs the shipped role split
+        (((6, 41),), y0),  # conv_s2w: layer2 one tile per workgroup, layer3 prefetch distance 2
+        (((6, 42),), y0),  # conv_s2w: layer2 prefetch distance 2
+        (((6, 44),), y0),  # conv_s2w: XCD-aware order off
+        (((6, 3),), ys2x),  # the one-tile stride-2 kernel (conv_s2.hip) on every entry
+        (((6, 11),), ys2x),  # conv_s2x: one tile per workgroup (layer2: the round-2a 8x16 kernel)
+        (((6, 26),), ys2x),  # conv_s2x multi-tile workgroups: layer2 4 waves of 32x64; layer3 as shipped
+        (((6, 27),), ys2x),  # conv_s2x layer2 prefetch distance 3; layer3 two 4x16 tiles per workgroup
+    )
+    for vs, ref in sets:
+        assert torch.equal(run(vs), ref), vs
 
 
 def test_forward_into_out_buffer():

@@ -52,13 +52,13 @@ def _truth(n, ticks, seed=5):
     constant body angular velocity w and world velocity v.  Returns poses (ticks, n) of
     (R, t), w (n, 3), v (n, 3)."""
     rng = np.random.default_rng(seed)
-    w = 0.4 * rng.standard_normal((n, 3))
-    v = 0.04 * rng.standard_normal((n, 3))
+    w = 0.3 * rng.standard_normal((n, 3))
+    v = 0.01 * rng.standard_normal((n, 3))
     poses = []
     cur = []
     for c in range(n):
         R0, _ = F.pose_exp(np.concatenate([0.3 * rng.standard_normal(3), np.zeros(3)]))
-        cur.append((R0, np.array([0.01, -0.02, 0.35]) + 0.01 * rng.standard_normal(3)))
+        cur.append((R0, np.array([0.0, 0.0, 0.35]) + 0.005 * rng.standard_normal(3)))
     for _ in range(ticks):
         poses.append(list(cur))
         cur = [F.compose(T, F.pose_exp(np.concatenate([DT * w[c], DT * (T[0].T @ v[c])]))) for c, T in enumerate(cur)]
