@@ -34,13 +34,19 @@
 
 namespace pa {
 
-// issue schedule per wave (compile time): U units of 10 steps
+// issue schedule per wave (compile time): U units of 10 steps.  x3: units are fp16x3 virtual
+// blocks (x_hi w_hi, x_hi w_lo, x_lo w_hi per 64 channels): the second one reads the patch
+// the first one loaded, so it loads nothing (ld)
 struct S2wPlan {
-  int nsteps, nunits, pd, wdma, po, pe, rl, rs, ut, nstore;  // ut = units per tile, rs = epilogue-load lead
+  int nsteps, nunits, pd, wdma, po, pe, rl, rs, ut, nstore, x3;  // ut = units per tile, rs = epilogue-load lead
+  constexpr bool ld(int u) const { return !x3 || (u % ut) % 3 != 1; }  // unit u loads its own patch
+  constexpr int src(int u) const { return ld(u) ? u : u - 1; }          // the unit whose patch u reads
   constexpr int ns(int t) const { return (t > 0 && t % (10 * ut) == 0) ? nstore : 0; }  // previous tile's stores
   constexpr int nw(int t) const { return t + pd < nsteps ? wdma : 0; }
-  constexpr int npo(int t) const { return (t % 10 == 0 && t / 10 >= 1) ? po : 0; }               // odd rows, this unit
-  constexpr int npe(int t) const { return (t % 10 == 4 && t / 10 + 1 < nunits) ? pe : 0; }        // even rows, next unit
+  constexpr int npo(int t) const { return (t % 10 == 0 && t / 10 >= 1 && ld(t / 10)) ? po : 0; }  // odd rows, this unit
+  constexpr int npe(int t) const {  // even rows, next unit
+    return (t % 10 == 4 && t / 10 + 1 < nunits && ld(t / 10 + 1)) ? pe : 0;
+  }
   constexpr int nr(int t) const { return (t + rs) % (10 * ut) == 0 ? rl : 0; }  // rs steps before each tile's end
   constexpr int cum(int t) const {
     int c = 0;
@@ -56,7 +62,7 @@ struct S2wPlan {
       const int t = v - pd;
       need = before(t) + ns(t) + nw(t);
     }
-    const int u = v / 10, tv = v % 10;
+    const int u = src(v / 10), tv = v % 10;
     if (tv < 4 && u >= 1) {  // even rows of unit u, DMA'd at unit u - 1's step 4
       const int t = (u - 1) * 10 + 4;
       const int e = before(t) + ns(t) + nw(t) + npo(t) + npe(t);
@@ -85,8 +91,11 @@ __host__ __device__ constexpr int s2w_kw(int t) { return t < 3 ? t : (t == 3 ? 1
 typedef unsigned s2w_u4 __attribute__((ext_vector_type(4)));
 constexpr unsigned S2W_OOB = 0x80000000u;
 __device__ __forceinline__ s2w_u4 s2w_rsrc(const void* base, unsigned bytes) {
+  // wave-uniform by construction; readfirstlane puts it in SGPRs for the asm's "s" operand
   const unsigned long long b = (unsigned long long)base;
-  return s2w_u4{(unsigned)b, (unsigned)(b >> 32) & 0xffffu, bytes, 0x00020000u};
+  return s2w_u4{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)b),
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32) & 0xffffu),
+                (unsigned)__builtin_amdgcn_readfirstlane(bytes), 0x00020000u};
 }
 __device__ __forceinline__ void s2w_dma16(s2w_u4 rsrc, unsigned voff, char* lds) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -99,12 +108,18 @@ __device__ __forceinline__ void s2w_dma16(s2w_u4 rsrc, unsigned voff, char* lds)
 #endif
 }
 
-template <int BN, int WM, int WN, int CIN, int PD, int TPW, bool WT = true>
+// X3 (fp16x3 parity mode, conv_gx.h X3): activation planes [hi (CIN) | lo (CIN)] per pixel,
+// weights hi / lo planes of w * 2^e; a unit is one of the 3 virtual blocks per 64 channels
+// (GxBlocks), the epilogue unscales exactly and writes (hi, lo) plane pairs.
+template <int BN, int WM, int WN, int CIN, int PD, int TPW, bool WT = true, bool X3 = false>
 __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg) {
   constexpr int TH = 8, TW = 16;
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int NCB = CIN / 64;
-  constexpr int NU = TPW * NCB;      // units (tile, 64-channel block) in the stream
+  using VB = GxBlocks<X3, NCB>;
+  constexpr int XS = X3 ? 2 : 1;     // fp16 planes per element
+  constexpr int NVB = VB::NVB;       // units per tile
+  constexpr int NU = TPW * NVB;      // units (tile, virtual 64-channel block) in the stream
   constexpr int NSTEPS = NU * 10;
   constexpr int PW = 2 * TW + 1;     // LDS positions per patch row: 17 even-local + 16 odd-local columns
   constexpr int RO = TH + 1, RE = TH;  // odd / even region rows
@@ -123,13 +138,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
   constexpr int NSLOT = PD + 1;  // one barrier per step
   constexpr int RL = 0;  // bias / bias2 are staged in LDS by the prologue (32 VGPRs not held across the stream)
   constexpr int RSD = 4;
-  constexpr int NST = TM * (TN / 2) * 2;  // output stores per tile (out, out2)
-  constexpr S2wPlan plan{NSTEPS, NU, PD, WDMA, PO, PE, RL, RSD, NCB, NST};
-  static_assert(PATCHB + NSLOT * WB + 2 * BN * 4 <= 163840, "LDS");
-  __shared__ __attribute__((aligned(1024))) char smem[PATCHB + NSLOT * WB + 2 * BN * 4];
+  constexpr int NST = TM * (TN / 2) * 2 * XS;  // output stores per tile (out, out2; hi, lo)
+  constexpr S2wPlan plan{NSTEPS, NU, PD, WDMA, PO, PE, RL, RSD, NVB, NST, X3 ? 1 : 0};
+  constexpr int EB = 2 * XS * BN * 4;  // epilogue constants: bias, bias2 (X3: scale, scale2)
+  static_assert(PATCHB + NSLOT * WB + EB <= 163840, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[PATCHB + NSLOT * WB + EB];
   char* patch = smem;
   char* wring = smem + PATCHB;
-  float* bl = reinterpret_cast<float*>(smem + PATCHB + NSLOT * WB);  // [bias (BN) | bias2 (BN)]
+  float* bl = reinterpret_cast<float*>(smem + PATCHB + NSLOT * WB);  // [bias | bias2 | scale | scale2] (BN each)
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
@@ -166,7 +182,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
   auto dma_region = [&](int u, auto ev) __attribute__((always_inline)) {
     constexpr bool even = decltype(ev)::value;
     constexpr int rows = even ? RE : RO, base = even ? POS_E : 0, npc = even ? PE : PO;
-    const int j = u / NCB, cb = u - (u / NCB) * NCB;
+    const int j = u / NVB, vb = u - (u / NVB) * NVB;
+    const int boff = gx_boff<NCB, CIN>(VB::pblk(vb));  // element offset of the unit's plane block
     int th0, tw0;
     tile_origin(j, th0, tw0);
     // the per-lane index made opaque per call: the address arithmetic is redone at every
@@ -174,7 +191,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
     // K loop
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const s2w_u4 rs = s2w_rsrc(in + (size_t)img * Hin * Win * CIN, (unsigned)(Hin * Win * CIN * 2));
+    const s2w_u4 rs = s2w_rsrc(in + (size_t)img * Hin * Win * XS * CIN, (unsigned)(Hin * Win * XS * CIN * 2));
 #pragma unroll
     for (int i = 0; i < npc; ++i) {
       const int c = (i * NW + wid) * 64 + ln;
@@ -185,7 +202,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
       const int col = pos <= TW ? 2 * pos : 2 * (pos - TW - 1) + 1;
       const int h = 2 * th0 + (even ? 2 * pr : 2 * pr - 1), x = 2 * tw0 - 1 + col;
       const bool ok = pr < rows && (unsigned)h < (unsigned)Hin && (unsigned)x < (unsigned)Win;
-      const unsigned vo = ok ? (unsigned)(((h * Win + x) * CIN + cb * 64 + lc * 8) * 2) : S2W_OOB;
+      const unsigned vo = ok ? (unsigned)(((h * Win + x) * XS * CIN + boff + lc * 8) * 2) : S2W_OOB;
       s2w_dma16(rs, vo, patch + base * 128 + (i * NW + wid) * 1024);
     }
   };
@@ -196,14 +213,15 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
   for (int i = 0; i < WDMA; ++i) {
     const int c = (i * NW + wid) * 64 + lane;
     const int co = c >> 3, lc = (c & 7) ^ ((co >> 1) & 7);
-    wsrc[i] = w + (size_t)(n0 + xperm(co)) * (9 * CIN) + lc * 8;
-    dsrc[i] = wds + (size_t)(n0 + xperm(co)) * CIN + lc * 8;
+    wsrc[i] = w + (size_t)(n0 + xperm(co)) * (9 * XS * CIN) + lc * 8;
+    dsrc[i] = wds + (size_t)(n0 + xperm(co)) * XS * CIN + lc * 8;
   }
   auto dma_w = [&](int s) __attribute__((always_inline)) {
-    const int t = s % 10, cb = (s / 10) % NCB, tap = s2w_tap(t);
+    const int t = s % 10, vb = (s / 10) % NVB, tap = s2w_tap(t);
+    const int wo = gx_boff<NCB, CIN>(VB::wblk(vb));
 #pragma unroll
     for (int i = 0; i < WDMA; ++i) {
-      const _Float16* src = tap >= 0 ? wsrc[i] + tap * CIN + cb * 64 : dsrc[i] + cb * 64;
+      const _Float16* src = tap >= 0 ? wsrc[i] + tap * XS * CIN + wo : dsrc[i] + wo;
       xdma16(src, wring + (s % NSLOT) * WB + (i * NW + wid) * 1024);
     }
   };
@@ -230,6 +248,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
   if (tid < BN) {
     bl[tid] = a.bias[n0 + tid];
     bl[BN + tid] = a.bias2[n0 + tid];
+    if constexpr (X3) {
+      bl[2 * BN + tid] = a.scale[n0 + tid];
+      bl[3 * BN + tid] = a.scale2[n0 + tid];
+    }
   }
   __builtin_amdgcn_sched_barrier(0);
   dma_region(0, std::false_type{});
@@ -249,21 +271,39 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
     for (int tm = 0; tm < TM; ++tm) {
       const int m = wm * WTM + tm * 16 + o;
       const int y = m / TW, x = m - (m / TW) * TW;
-      const size_t pixo = (((size_t)img * H + th0 + y) * W + tw0 + x) * Cout + n0 + wn * WTN + q * 8;
+      const size_t pixo = (((size_t)img * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
 #pragma unroll
       for (int p = 0; p < TN / 2; ++p) {
         // this lane's 8 channels wn * WTN + p * 32 + q * 8 .. + 7 (tiles 2p, 2p + 1)
         const f32x4* b4 = reinterpret_cast<const f32x4*>(bl + wn * WTN + p * 32 + q * 8);
         const f32x4 b0 = b4[0], b1 = b4[1], d0 = b4[BN / 4], d1 = b4[BN / 4 + 1];
-        half8 h1, h2;
+        half8 h1, h2, l1, l2;
+        if constexpr (X3) {
+          const f32x4 s0 = b4[BN / 2], s1 = b4[BN / 2 + 1], t0 = b4[3 * BN / 4], t1 = b4[3 * BN / 4 + 1];
 #pragma unroll
-        for (int e8 = 0; e8 < 8; ++e8) {
-          const int tn = 2 * p + (e8 >> 2), e = e8 & 3;
-          h1[e8] = (_Float16)fmaxf(acc[tm][tn][e] + (e8 < 4 ? b0 : b1)[e], 0.f);
-          h2[e8] = (_Float16)(accd[tm][tn][e] + (e8 < 4 ? d0 : d1)[e]);
+          for (int e8 = 0; e8 < 8; ++e8) {
+            const int tn = 2 * p + (e8 >> 2), e = e8 & 3;
+            const HiLo a1 = split_x3(fmaxf(acc[tm][tn][e] * (e8 < 4 ? s0 : s1)[e] + (e8 < 4 ? b0 : b1)[e], 0.f));
+            const HiLo a2 = split_x3(accd[tm][tn][e] * (e8 < 4 ? t0 : t1)[e] + (e8 < 4 ? d0 : d1)[e]);
+            h1[e8] = a1.hi;
+            l1[e8] = a1.lo;
+            h2[e8] = a2.hi;
+            l2[e8] = a2.lo;
+          }
+        } else {
+#pragma unroll
+          for (int e8 = 0; e8 < 8; ++e8) {
+            const int tn = 2 * p + (e8 >> 2), e = e8 & 3;
+            h1[e8] = (_Float16)fmaxf(acc[tm][tn][e] + (e8 < 4 ? b0 : b1)[e], 0.f);
+            h2[e8] = (_Float16)(accd[tm][tn][e] + (e8 < 4 ? d0 : d1)[e]);
+          }
         }
         store16<WT>(out, (unsigned)((pixo + p * 32) * 2), h1);
         store16<WT>(out2, (unsigned)((pixo + p * 32) * 2), h2);
+        if constexpr (X3) {
+          store16<WT>(out, (unsigned)((pixo + Cout + p * 32) * 2), l1);
+          store16<WT>(out2, (unsigned)((pixo + Cout + p * 32) * 2), l2);
+        }
       }
     }
   };
@@ -301,9 +341,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
     constexpr int S = decltype(sc)::value;
     constexpr int U = S / 10, T = S % 10;
     using DS = std::integral_constant<bool, T == 3>;
-    if constexpr (S > 0 && S % (10 * NCB) == 0) {  // previous tile done: its stores (plan.ns), fresh accumulators
+    if constexpr (S > 0 && S % (10 * NVB) == 0) {  // previous tile done: its stores (plan.ns), fresh accumulators
       __builtin_amdgcn_sched_barrier(0);
-      epilogue(S / (10 * NCB) - 1);
+      epilogue(S / (10 * NVB) - 1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -321,8 +361,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
     // DMAs after this step's LDS reads (see xdma16); order = S2wPlan's
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (S + PD < NSTEPS) dma_w(S + PD);
-    if constexpr (T == 0 && U >= 1) dma_region(U, std::false_type{});       // this unit's odd rows (read from its step 4)
-    if constexpr (T == 4 && U + 1 < NU) dma_region(U + 1, std::true_type{});  // the next unit's even rows (this unit's are done)
+    if constexpr (T == 0 && U >= 1 && plan.ld(U)) dma_region(U, std::false_type{});  // this unit's odd rows (read from its step 4)
+    if constexpr (T == 4 && U + 1 < NU && plan.ld(U + 1))
+      dma_region(U + 1, std::true_type{});  // the next unit's even rows (this unit's are done)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
     mfma(xic<1>{}, DS{});
@@ -337,9 +378,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
   epilogue(TPW - 1);
 }
 
-template <int BN, int WM, int WN, int CIN, int PD, int TPW, bool WT = true>
+template <int BN, int WM, int WN, int CIN, int PD, int TPW, bool WT = true, bool X3 = false>
 static int run_s2w(const ConvS2Args& a, bool xg, hipStream_t s) {
-  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 < 0x7fffffffu, "s2w conv: output over 2 GB");
+  PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "s2w conv: output over 2 GB");
+  PA_CHECK(!X3 || (a.scale && a.scale2), "s2w conv (fp16x3): scales required");
   PA_CHECK(a.Cin == CIN, "s2w conv: Cin %d != %d", a.Cin, CIN);
   PA_CHECK(a.Hin == 2 * a.Hout && a.Win == 2 * a.Wout, "s2w conv: %dx%d -> %dx%d", a.Hin, a.Win, a.Hout, a.Wout);
   PA_CHECK(a.Hout % 8 == 0 && a.Wout % 16 == 0, "s2w conv: %dx%d not tiled by 8x16", a.Hout, a.Wout);
@@ -349,7 +391,7 @@ static int run_s2w(const ConvS2Args& a, bool xg, hipStream_t s) {
   const int ntn = a.Cout / BN;
   const int nsp = a.B * (a.Hout / 8) * (a.Wout / 16) / TPW;
   const int x = xg && nsp % 8 == 0;
-  hipLaunchKernelGGL((conv3x3s2_w<BN, WM, WN, CIN, PD, TPW, WT>), dim3(nsp * ntn), dim3(WM * WN * 64), 0, s, a, x);
+  hipLaunchKernelGGL((conv3x3s2_w<BN, WM, WN, CIN, PD, TPW, WT, X3>), dim3(nsp * ntn), dim3(WM * WN * 64), 0, s, a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

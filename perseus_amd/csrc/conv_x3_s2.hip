@@ -1,19 +1,37 @@
-// conv_s2x.h X3 (fp16x3 parity mode) instantiations: the stride-2 + downsample entry
-// conv of layers 2-4, same tiles as the fp16 kernels (conv_s2x_l.hip).
+// fp16x3 (parity mode) stride-2 + downsample entry convs.  Layers 2 / 3: conv_s2w.h's
+// 8 x 16 x 128 tiles with the row-split patch (shipped; the x_hi patch is staged once for
+// its two products); layer4 and the A/B forms: conv_s2x.h (conv_s2x_l.hip's tiles).
+#include "conv_s2w.h"
 #include "conv_s2x.h"
 
 namespace pa {
 
 int launch_conv3x3s2_x3(const ConvS2Args& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
+  const int v = g_variant[6];
+  const bool s2x = v == 44 || v == 45;  // conv_s2x.h forms (A/B; 45 = its shipped tiles)
   if (a.Hout == 32 && a.Cin == 64) {
+    if (!s2x) {
+      // 64-channel tiles (the 128-channel X3 tile spills 43-110 VGPRs), two per workgroup (variant 46: one):
+      // 49.5 / 52.2 us against 57.8 for conv_s2x.h (profiles/r04e/)
+      if (kname) *kname = "conv3x3s2w3_l2";
+      if (v == 46) return run_s2w<64, 4, 2, 64, 3, 1, true, true>(a, true, s);
+      return run_s2w<64, 4, 2, 64, 3, 2, true, true>(a, true, s);
+    }
     if (kname) *kname = "conv3x3s2x3_l2";
     // 8 waves of 32 x 32 (210 VGPRs): 55.1 us against 60.9 for 4 waves of 32 x 64 (366 VGPRs, one
     // wave per SIMD, variant 44); multi-tile workgroups spill here (85 / 77 us)
-    if (g_variant[6] == 44) return run_s2x<4, 16, 128, 2, 2, 64, 3, 1, true, true>(a, true, s);
+    if (v == 44) return run_s2x<4, 16, 128, 2, 2, 64, 3, 1, true, true>(a, true, s);
     return run_s2x<4, 16, 128, 2, 4, 64, 3, 1, true, true>(a, true, s);  // 2 patch buffers: 4-row tile
   }
   if (a.Hout == 16 && a.Cin == 128) {
+    if (!s2x) {
+      if (kname) *kname = "conv3x3s2w3_l3";
+      // two tiles per workgroup (4 VGPRs spilled; 43.9 vs 45.2 us for one, variant 46, and 47.4 for
+      // conv_s2x.h, profiles/r04e/)
+      if (v == 46) return run_s2w<64, 4, 2, 128, 3, 1, true, true>(a, true, s);
+      return run_s2w<64, 4, 2, 128, 3, 2, true, true>(a, true, s);
+    }
     if (kname) *kname = "conv3x3s2x3_l3";
     return run_s2x<4, 16, 128, 2, 4, 128, 3, 1, true, true>(a, true, s);
   }

@@ -144,7 +144,7 @@ def test_fp16x3_profile_and_precision_switch():
     prof, y = m.profile(x)
     names = [n for n, _ in prof]
     assert names[0] == "stem_x3_conv7x7_pool" and names[-1] == "avgpool_fc_x3" and len(names) == 18
-    assert names[5] == "conv3x3s2x3_l2" and names[1] == "conv3x3x3_l1"
+    assert names[5] == "conv3x3s2w3_l2" and names[9] == "conv3x3s2w3_l3" and names[1] == "conv3x3x3_l1"
     assert torch.equal(y, m(x))
     m.precision = "fp16"
     y16 = m(x)
@@ -314,17 +314,34 @@ def test_profile_reports_every_kernel():
     assert [n for n, _ in prof32][:2] == ["stem_conv7x7", "maxpool"]
 
 
-def test_fp16x3_stride2_variants_agree_bit_for_bit():
-    """fp16x3: the layer2 stride-2 entry's 8-wave tile (shipped) against the 4-wave one."""
+def test_fp16x3_stride2_variants_agree_bit_for_bit(gold):
+    """fp16x3 stride-2 entries: the shipped row-split kernel (conv_s2w.h X3) against its
+    one- / two-tile workgroup variant (same sum order: bit for bit); conv_s2x.h's 8-wave
+    tile (variant 45) against its 4-wave one (44), bit for bit; and the two kernel families
+    (taps summed in another order) within f32 rounding, both at the golden outputs' 1e-3 px."""
     m = model(0, precision="fp16x3")
     x = torch.from_numpy(synth.synthetic_frames(4, 5)).cuda()
-    y0 = m(x)
-    try:
-        m.set_variants({6: 44})
-        y1 = m(x)
-    finally:
-        m.set_variants({})
-    assert torch.equal(y0, y1)
+
+    def run(v):
+        try:
+            m.set_variants({6: v})
+            return m(x)
+        finally:
+            m.set_variants({})
+
+    y0, y46, y45, y44 = m(x), run(46), run(45), run(44)
+    assert torch.equal(y0, y46)
+    assert torch.equal(y45, y44)
+    assert (y0 - y45).abs().max().item() * PX <= 1e-4
+    name, seed, xg = cases()[0]
+    mg = model(seed, precision="fp16x3")
+    for v in (0, 45):
+        try:
+            mg.set_variants({6: v} if v else {})
+            y = mg(torch.from_numpy(xg).cuda()).cpu().numpy()
+        finally:
+            mg.set_variants({})
+        assert np.abs(y - gold[f"{name}/y_ref_f32"]).max() * PX <= FP32_PX_MAX
 
 
 def test_fp16x3_merged_steps_match_three_block_form(gold):
