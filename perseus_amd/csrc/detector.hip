@@ -393,6 +393,10 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       if (small_s2) {
         sa.part = d->part;
         PA_RUN(launch_conv3x3s2_small(sa, s, &kn), kn);
+      } else if (std::is_same<T, _Float16>::value && small && ho == 16 && g_variant[6] == 0) {
+        // layer3's entry in the latency mode: conv_s2x.h's 4 x 16 tiles (twice the workgroups of
+        // the batched conv_s2w.h tiles at a few frames: 24 vs 12 at B = 3)
+        PA_RUN(launch_conv3x3s2_x(sa, 0, s, &kn), kn);
       } else {
         PA_RUN(launch_conv3x3s2_ds<T>(sa, s, &kn), kn);
       }
