@@ -211,7 +211,9 @@ int pa_trajectory_linearize(const pa_traj_args* args, void* stream);
  * solves (J^T J + lambda I) delta = -J^T r.  Outputs: D (T*L, 12, 12) diagonal and
  * E (T*(L-1), 12, 12) off-diagonal blocks of J^T J (E_l couples frame l rows with
  * frame l+1 columns), g (T*L, 12) = J^T r, delta (T*L, 12), info (T) = 0 or the
- * 1-based frame whose pivot block was not positive definite (delta NaN).  D, E and g
+ * 1-based frame of a pivot block found not positive definite (delta NaN; which frame
+ * depends on the elimination order: launches of few trajectories with L <= 24 run block
+ * cyclic reduction, others a two-ended block elimination).  D, E and g
  * may all be NULL (then the blocks stay on chip: the step's HBM traffic is the factors in
  * and delta out).  Projection factors with status != 0 (cheirality, or a frame outside a
  * window's filled part) are skipped; with n_kp = 0 r_proj / j_proj may be NULL.

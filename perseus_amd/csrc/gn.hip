@@ -16,7 +16,9 @@
 // operator, run from both ends).  Kept as variants (gn_step_kernel): SOLVER 1, the same
 // elimination as one top-down chain fed by NA assembler waves; SOLVER 0, the round-2 block
 // Cholesky (L_l L_l^T = D_l + lambda I - W_l^T W_l, W_l = L_{l-1}^{-1} E_{l-1}) with
-// forward and back substitution.  D / E / g are also written out (the API's outputs).
+// forward and back substitution.  Launches of at most as many trajectories as CUs (the
+// streaming tick's T = 3) with L <= 24 run gn_cr_kernel instead: block cyclic reduction,
+// 5 serial pivots at L = 24 instead of 13.  D / E / g are optional outputs.
 // f64 throughout.
 // Jacobians are column-major per factor (include/perseus_amd.h).
 #include "common.h"
@@ -1054,6 +1056,277 @@ __global__ __launch_bounds__(256, OCC) void gn_twisted_kernel(GnArgs a) {
   gn_stamp(a, t, 251);
 }
 
+// ---------------------------------------------------------------- cyclic reduction (few trajectories)
+// At T = 3 (the streaming tick) the two-ended elimination above is a 13-frame serial chain on
+// 3 CUs.  Block cyclic reduction cuts the serial depth to log2(L) levels by eliminating every
+// other active frame at once.  One workgroup of 12 waves per trajectory, all blocks in LDS:
+//   assembly   the waves build frames w, w + NS, .. (gn_build_frame) straight into fb[l] = D | E | g,
+//              then S_l = D_l + lambda I, b_l = -g_l, C_l = E_l (the coupling to the next
+//              active frame)
+//   level      active frames a_0 .. a_{n-1}; n even: the odd positions are eliminated, n odd:
+//              the even ones (so every eliminated frame's neighbours survive).  Eliminated i
+//              with neighbours p < i < q (either may be absent):
+//                M_i = S_i^-1 (gn_sweep: the PD test of the pivot), z_i = M_i b_i,
+//                PM_i = C_p M_i,  QM_i = C_i^T M_i                    (one wave each)
+//              then each survivor s with eliminated neighbours h < s < i and next survivor q:
+//                S_s -= QM_h C_h + PM_i C_s^T,  b_s -= C_h^T z_h + C_s z_i,
+//                C_s <- -PM_i C_i                                     (one wave each)
+//   last       n = 1: delta = S^-1 b
+//   back       levels in reverse: delta_i = z_i - PM_i^T delta_p - QM_i^T delta_q.
+// L = 24: 5 sweeps in series (24 -> 12 -> 6 -> 3 -> 1 -> solve) instead of 13; about twice
+// the flops of the elimination, so it is the form for launches that leave CUs idle.  The
+// 12 x 12 products run on the f64 matrix cores.  info: the 1-based frame of the first
+// level's (lowest) pivot block that is not positive definite, 0 = solved.
+constexpr int GN_CR_LMAX = 24;
+constexpr int GN_CR_W = 12;  // waves per workgroup
+typedef double gn_d4 __attribute__((ext_vector_type(4)));
+
+// acc += A B for 12 x 12 row-major LDS blocks (A read transposed when TA, B when TB), on the
+// f64 matrix cores: A operand lane l = (row l & 15, k = l >> 4), B operand (k = l >> 4,
+// column l & 15), result register v = (row (l >> 4) + 4 v, column l & 15); rows / columns
+// 12..15 are zero padding
+template <bool TA, bool TB>
+__device__ __forceinline__ gn_d4 gn_mm_acc(const double* A, const double* B, gn_d4 acc) {
+  using namespace gn;
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const bool in = li < NV;
+  const int lr = in ? li : 0;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int k = 4 * q + lk;
+    const double av = in ? (TA ? A[k * NV + lr] : A[lr * NV + k]) : 0.0;
+    const double bv = in ? (TB ? B[lr * NV + k] : B[k * NV + lr]) : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// a C-layout result to a 12 x 12 row-major LDS block (scaled by s)
+__device__ __forceinline__ void gn_mm_store(double* out, const gn_d4& c, double s) {
+  using namespace gn;
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  if (li < NV)
+#pragma unroll
+    for (int v = 0; v < 3; ++v) out[(lk + 4 * v) * NV + li] = s * c[v];
+}
+
+template <int RP, int NS>
+__global__ __launch_bounds__(64 * GN_CR_W, 1) void gn_cr_kernel(GnArgs a) {
+  using namespace gn;
+  constexpr int BLK = 2 * NB + NV;
+  constexpr int LM = GN_CR_LMAX, W = GN_CR_W;
+  constexpr int CHD = (int)(sizeof(GnChainLds) / sizeof(double));
+  constexpr int STGD = (int)(sizeof(GnStage<RP>) / sizeof(double));
+  constexpr int FR = 2 * NB + NV;  // per eliminated frame: PM | QM | z
+  // PAIR (one assembler wave per two frames, NS = W): wave w builds frames 2w, 2w + 1 and
+  // eliminates 2w + 1 at once (level 0 eliminates the odd positions whatever L's parity), so
+  // level 0 needs no barrier of its own.  Its slab of the pool is its staging, then the
+  // PM | QM | z of frames 2w + 1 and 2w and its sweep scratch.  Otherwise (the general-K
+  // instance: its staging does not fit 12 times) NS waves assemble, then every wave starts.
+  constexpr bool PAIR = NS == W && 2 * W >= LM;
+  constexpr int SLAB0 = 2 * FR + CHD > STGD ? 2 * FR + CHD : STGD;
+  constexpr int SLAB = (SLAB0 + 1) / 2 * 2;
+  constexpr int POST = LM * FR + W * CHD;
+  constexpr int STG = NS * STGD;
+  constexpr int POOL = PAIR ? W * SLAB : (POST > STG ? POST : STG);
+  constexpr int NOFAIL = 0x7fffffff;
+  static_assert(NS <= W, "assembler waves");
+  __shared__ __attribute__((aligned(16))) double fb[LM][BLK];  // S | C | b per frame (delta over S at the end)
+  __shared__ __attribute__((aligned(16))) double pool[POOL];   // assembly staging, then the level data
+  __shared__ signed char lst[8][LM];                           // active frames per level
+  __shared__ int lcnt[8], lpe[8];
+  __shared__ int nlev_s, fail;
+  const int t = blockIdx.x;
+  const int wv = threadIdx.x >> 6;
+  const int i = threadIdx.x & 63;
+  const int L = a.L;
+  const long f0 = (long)t * L;
+  auto fr = [&](int f) __attribute__((always_inline)) -> double* {  // PM | QM | z of frame f
+    return PAIR ? pool + (f >> 1) * SLAB + ((f & 1) ? 0 : FR) : pool + f * FR;
+  };
+  GnChainLds& C = *reinterpret_cast<GnChainLds*>(PAIR ? pool + wv * SLAB + 2 * FR : pool + LM * FR + wv * CHD);
+  auto dl = [&](int f) __attribute__((always_inline)) -> double* { return fb[f]; };
+  if (threadIdx.x == 0) {
+    int n = L, lv = 0;
+    for (int l = 0; l < L; ++l) lst[0][l] = (signed char)l;
+    while (n > 1) {
+      const int pe = (PAIR && lv == 0) || !(n & 1) ? 1 : 0;  // parity of the eliminated positions
+      int m = 0;
+      for (int p = 0; p < n; ++p)
+        if ((p & 1) != pe) lst[lv + 1][m++] = lst[lv][p];
+      lcnt[lv] = n;
+      lpe[lv] = pe;
+      n = m;
+      ++lv;
+    }
+    lcnt[lv] = 1;
+    nlev_s = lv;
+    fail = NOFAIL;
+  }
+  if (wv == 0) gn_stamp(a, t, 0);
+  const bool act = i < 36;
+  const int ii = act ? i : 35;
+  const int r = ii / 3, c0 = 4 * (ii - 3 * (ii / 3));
+  // eliminate frame fi (neighbours fp, fq, or -1): M = S^-1 (false if S is not PD), z = M b,
+  // PM = C_p M, QM = C_fi^T M
+  auto eliminate = [&](int fi, int fp, int fq) __attribute__((always_inline)) {
+    double sv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sv[c] = fb[fi][r * NV + c0 + c];
+    const double b = fb[fi][2 * NB + r];
+    if (!gn_sweep(sv, C.rk2, r, c0, act)) {
+      if (i == 0) __hip_atomic_fetch_min(&fail, fi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
+    double* o = fr(fi);
+    const double z = gn_finish(sv, b, C, r, c0, act);  // C.M = M
+    if (act && c0 == 0) o[2 * NB + r] = z;
+    if (fp >= 0) gn_mm_store(o, gn_mm_acc<false, false>(fb[fp] + NB, C.M, gn_d4{0, 0, 0, 0}), 1.0);
+    if (fq >= 0) gn_mm_store(o + NB, gn_mm_acc<true, false>(fb[fi] + NB, C.M, gn_d4{0, 0, 0, 0}), 1.0);
+  };
+  // S = D + lambda I, b = -g (frame l; lanes < 12 of one wave)
+  auto init = [&](int l) __attribute__((always_inline)) {
+    if (i < NV) {
+      fb[l][i * NV + i] += a.lambda;
+      fb[l][2 * NB + i] = -fb[l][2 * NB + i];
+    }
+  };
+  if constexpr (PAIR) {
+    // ---- wave w: frames 2w, 2w + 1 (both loads issued before either is built), then the
+    // level-0 elimination of 2w + 1
+    const int la = 2 * wv, lb = 2 * wv + 1;
+    if (la < L) {
+      GnStage<RP>& st = *reinterpret_cast<GnStage<RP>*>(pool + wv * SLAB);
+      gn_zero_stage<RP>(st);
+      GnFrameLoads<RP> ld0, ld1;
+      gn_load_frame<RP>(a, f0 + la, ld0);
+      if (lb < L) gn_load_frame<RP>(a, f0 + lb, ld1);
+      gn_build_frame<RP, false>(a, f0 + la, ld0, st, fb[la]);
+      if (lb < L) gn_build_frame<RP, false>(a, f0 + lb, ld1, st, fb[lb]);
+      wave_order();
+      init(la);
+      if (lb < L) init(lb);
+      wave_order();
+      if (wv == 0) gn_stamp(a, t, 2);
+      if (lb < L) eliminate(lb, la, lb + 1 < L ? lb + 1 : -1);  // (the staging is dead: the slab's new use)
+    }
+  } else {
+    if (wv < NS) {
+      GnStage<RP>& st = reinterpret_cast<GnStage<RP>*>(pool)[wv];
+      gn_zero_stage<RP>(st);
+      GnFrameLoads<RP> ld0;
+      if (wv < L) gn_load_frame<RP>(a, f0 + wv, ld0);
+      for (int l = wv; l < L; l += NS) {
+        const GnFrameLoads<RP> cu = ld0;
+        if (l + NS < L) gn_load_frame<RP>(a, f0 + l + NS, ld0);
+        gn_build_frame<RP, false>(a, f0 + l, cu, st, fb[l]);
+      }
+      if (wv == 0) gn_stamp(a, t, 2);
+    }
+    __syncthreads();
+    for (int l = wv; l < L; l += W) init(l);
+  }
+  const int nlev = nlev_s;
+  __syncthreads();
+  if (wv == 0) gn_stamp(a, t, 1);
+  int lv = 0;
+  for (; lv < nlev; ++lv) {
+    const int n = lcnt[lv], pe = lpe[lv];
+    const int ne = pe ? n / 2 : (n + 1) / 2;
+    if (!(PAIR && lv == 0)) {
+      for (int e = wv; e < ne; e += W) {  // eliminated frames
+        const int pos = 2 * e + pe;
+        eliminate(lst[lv][pos], pos > 0 ? lst[lv][pos - 1] : -1, pos + 1 < n ? lst[lv][pos + 1] : -1);
+      }
+      __syncthreads();
+    }
+    if (wv == 0) gn_stamp(a, t, 10 + 2 * lv);
+    if (fail != NOFAIL) break;
+    const int ns = n - ne;
+    for (int s = wv; s < ns; s += W) {  // survivors
+      const int pos = 2 * s + (1 - pe);
+      const int fs = lst[lv][pos];
+      const int fh = pos > 0 ? lst[lv][pos - 1] : -1;
+      const int fi = pos + 1 < n ? lst[lv][pos + 1] : -1;
+      const bool cq = fi >= 0 && pos + 2 < n;  // a next survivor: new coupling
+      gn_d4 acc = {0.0, 0.0, 0.0, 0.0}, cn = {0.0, 0.0, 0.0, 0.0};
+      if (fh >= 0) acc = gn_mm_acc<false, false>(fr(fh) + NB, fb[fh] + NB, acc);
+      if (fi >= 0) acc = gn_mm_acc<false, true>(fr(fi), fb[fs] + NB, acc);
+      if (cq) cn = gn_mm_acc<false, false>(fr(fi), fb[fi] + NB, cn);
+      double db0 = 0.0, db1 = 0.0;
+      if (i < NV) {
+        if (fh >= 0) {
+          const double* zh = fr(fh) + 2 * NB;
+#pragma unroll
+          for (int k = 0; k < NV; ++k) db0 += fb[fh][NB + k * NV + i] * zh[k];
+        }
+        if (fi >= 0) {
+          const double* zi = fr(fi) + 2 * NB;
+#pragma unroll
+          for (int k = 0; k < NV; ++k) db1 += fb[fs][NB + i * NV + k] * zi[k];
+        }
+      }
+      wave_order();  // this wave's reads of fb[fs] are issued before its writes
+      const int li = i & 15, lk = i >> 4;
+      if (li < NV)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) fb[fs][(lk + 4 * v) * NV + li] -= acc[v];
+      if (cq) gn_mm_store(fb[fs] + NB, cn, -1.0);
+      if (i < NV) fb[fs][2 * NB + i] -= db0 + db1;
+    }
+    __syncthreads();
+    if (wv == 0) gn_stamp(a, t, 11 + 2 * lv);
+  }
+  if (fail == NOFAIL && wv == 0) {  // the last active frame: delta = S^-1 b (over its S block)
+    const int ff = lst[nlev][0];
+    double sv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sv[c] = fb[ff][r * NV + c0 + c];
+    const double b = fb[ff][2 * NB + r];
+    if (!gn_sweep(sv, C.rk2, r, c0, act)) {
+      if (i == 0) __hip_atomic_fetch_min(&fail, ff + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      const double z = gn_finish(sv, b, C, r, c0, act);
+      wave_order();  // every lane's S reads are done
+      if (act && c0 == 0) dl(ff)[r] = z;
+    }
+  }
+  __syncthreads();
+  if (wv == 0) gn_stamp(a, t, 30);
+  const int info = fail == NOFAIL ? 0 : fail;
+  if (!info) {
+    for (lv = nlev - 1; lv >= 0; --lv) {  // delta_i over S_i's first row (dead since its elimination)
+      const int n = lcnt[lv], pe = lpe[lv];
+      const int ne = pe ? n / 2 : (n + 1) / 2;
+      for (int e = wv; e < ne; e += W) {
+        const int pos = 2 * e + pe;
+        const int fi = lst[lv][pos];
+        const int fp = pos > 0 ? lst[lv][pos - 1] : -1, fq = pos + 1 < n ? lst[lv][pos + 1] : -1;
+        const double* o = fr(fi);
+        if (i < NV) {
+          double d0 = o[2 * NB + i], d1 = 0.0;
+          if (fp >= 0)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) d0 -= o[k * NV + i] * dl(fp)[k];
+          if (fq >= 0)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) d1 += o[NB + k * NV + i] * dl(fq)[k];
+          dl(fi)[i] = d0 - d1;
+        }
+      }
+      __syncthreads();
+      if (wv == 0) gn_stamp(a, t, 31 + lv);
+    }
+  }
+  double* delta = a.delta + (size_t)f0 * NV;
+  for (int e = threadIdx.x; e < L * NV; e += 64 * W) {
+    const int l = e / NV;
+    delta[e] = info ? NAN : dl(l)[e - l * NV];
+  }
+  if (a.info && threadIdx.x == 0) a.info[t] = info;
+  if (wv == 0) gn_stamp(a, t, 40);
+}
+
 // assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * legacy;
 // 0 = the shipped choice)
 static int g_gn_na = 0;
@@ -1081,9 +1354,15 @@ static void launch_gn_sv(const GnArgs& a, int na, hipStream_t s) {
 
 // shipped: solver 2 (the two-ended elimination); v & 16 selects solver 1 (one top-down chain of
 // swept inverses) and v & 8 the round-2 block Cholesky, both with v & 7 assembler waves
+// cyclic reduction for launches of few trajectories (v & 64 forces it, v & 128 never)
 template <int RP>
 static void launch_gn(const GnArgs& a, int v, hipStream_t s) {
-  if (v & 8)
+  const bool cr_ok = a.L <= GN_CR_LMAX && !(v & 63);
+  // (T x 24, us, two-ended / cyclic: 3: 41.3 / 33.4, 64: 41.9 / 33.9, 256: 42.6 / 34.4,
+  // 512: 54.1 / 66.6, 1000: 71.3 / 130.8; profiles/r04i/gn_cr_ab.log)
+  if (cr_ok && ((v & 64) || (!(v & 128) && a.T <= g_gn_cus())))
+    hipLaunchKernelGGL((gn_cr_kernel<RP, RP <= 34 ? 12 : 8>), dim3(a.T), dim3(64 * GN_CR_W), 0, s, a);
+  else if (v & 8)
     launch_gn_sv<RP, 0>(a, v & 7, s);
   else if (v & 16)
     launch_gn_sv<RP, 1>(a, v & 7, s);
@@ -1103,9 +1382,10 @@ int pa_debug_gn_set_trace(unsigned long long* trace_dev) {
 }
 
 int pa_debug_gn_set_assemblers(int na) {
-  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 64 && !((na & 8) && (na & 16)),
+  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 256 && !((na & 8) && (na & 16)) && !((na & 64) && (na & 128)),
            "gn variant %d: assembler waves (0..4) + 8 * legacy Cholesky or 16 * single-chain solver, 32: "
-           "two-ended kernel in its 4-per-CU form", na);
+           "two-ended kernel in its 4-per-CU form, 64: cyclic reduction (L <= 24), 128: never cyclic "
+           "reduction", na);
   pa::g_gn_na = na;
   return PA_OK;
 }

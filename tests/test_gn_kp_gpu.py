@@ -17,14 +17,24 @@ S = 0.0175
 FACES = np.array([[S, 0, 0], [-S, 0, 0], [0, S, 0], [0, -S, 0], [0, 0, S], [0, 0, -S]])
 
 
-def _check(corners, T, L, lam, seed):
+def _check(corners, T, L, lam, seed, variant=None):
     K = len(corners)
     poses, vels, angvels, _ = _problem(T, L, seed)
     y = np.random.default_rng(seed + 1).uniform(-1, 1, (T * L, 2 * K)).astype(np.float32)
     lin = pipeline.linearize_trajectories(torch.as_tensor(y, device="cuda"), poses, vels, angvels, corners, KCAL,
                                           T=T, L=L, dt=0.1, proj_sigmas=np.array([2.0, 2.0]),
                                           dyn_sigmas=np.full(6, 0.05), cv_sigmas=np.full(3, 0.5))
-    out = pipeline.gn_step(lin, T=T, L=L, lam=lam)
+    if variant is None:
+        out = pipeline.gn_step(lin, T=T, L=L, lam=lam)
+    else:
+        from perseus_amd import _lib
+
+        L_ = _lib.lib()
+        try:
+            _lib.check(L_.pa_debug_gn_set_assemblers(variant))
+            out = pipeline.gn_step(lin, T=T, L=L, lam=lam)
+        finally:
+            _lib.check(L_.pa_debug_gn_set_assemblers(0))
     keys = ("r_proj", "j_proj", "status", "r_dyn", "j_dyn0", "j_dyn1", "j_dyn2", "j_dyn3", "r_cv", "j_cv0", "j_cv1")
     H, g, d = G.gn_step({k: lin[k].cpu().numpy() for k in keys}, T, L, K, lam)
     assert (out["info"].cpu().numpy() == 0).all()
@@ -75,7 +85,7 @@ def test_gn_step_more_trajectories_than_one_round():
 @pytest.mark.parametrize("variant", [16 + 2, 8 + 2])
 def test_gn_step_solver_variants_agree(variant):
     """The single-chain solver (16 + NA) and the round-2 block Cholesky (8 + NA), kept as
-    pa_debug_gn_set_assemblers variants, against the shipped two-ended kernel."""
+    pa_debug_gn_set_assemblers variants, against the shipped kernel (cyclic reduction at T = 4)."""
     from perseus_amd import _lib
 
     poses, vels, angvels, _ = _problem(4, 24, 3)
@@ -93,3 +103,39 @@ def test_gn_step_solver_variants_agree(variant):
     d0, d1 = ref["delta"].cpu().numpy(), out["delta"].cpu().numpy()
     np.testing.assert_allclose(d1, d0, rtol=1e-7, atol=1e-9 * np.abs(d0).max())
     assert torch.equal(ref["D"], out["D"]) and torch.equal(ref["g"], out["g"])
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 4, 5, 7, 13, 23, 24])
+@pytest.mark.parametrize("variant", [64, 128], ids=["cyclic", "two-ended"])
+def test_gn_step_cyclic_reduction_and_two_ended_forms(L, variant):
+    """Both solvers at every level shape of the cyclic reduction (n odd: the even positions are
+    eliminated, ends included; n even: the odd ones; L = 1: the last-frame solve alone), forced
+    through pa_debug_gn_set_assemblers (64: cyclic reduction, 128: the two-ended elimination)."""
+    _check(CORNERS, 3, L, 1e-3, 50 + L, variant)
+
+
+def test_gn_step_cyclic_reduction_many_trajectories():
+    """The cyclic-reduction kernel forced at 600 trajectories (several rounds of one
+    workgroup per CU)."""
+    _check(CORNERS, 600, 24, 1e-2, 6, 64)
+
+
+@pytest.mark.parametrize("variant", [64, 128], ids=["cyclic", "two-ended"])
+def test_gn_step_singular_in_both_forms(variant):
+    """lambda = 0: the last frame's angular velocity has no factor; both forms report that
+    frame (L) and NaN steps."""
+    from perseus_amd import _lib
+
+    T, L = 2, 6
+    poses, vels, angvels, y = _problem(T, L, 9)
+    lin = pipeline.linearize_trajectories(torch.as_tensor(y, device="cuda"), poses, vels, angvels, CORNERS, KCAL,
+                                          T=T, L=L, dt=0.1, proj_sigmas=np.array([2.0, 2.0]),
+                                          dyn_sigmas=np.full(6, 0.05), cv_sigmas=np.full(3, 0.5))
+    L_ = _lib.lib()
+    try:
+        _lib.check(L_.pa_debug_gn_set_assemblers(variant))
+        out = pipeline.gn_step(lin, T=T, L=L, lam=0.0)
+    finally:
+        _lib.check(L_.pa_debug_gn_set_assemblers(0))
+    assert (out["info"].cpu().numpy() == L).all()
+    assert torch.isnan(out["delta"]).all()

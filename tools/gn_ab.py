@@ -1,8 +1,9 @@
 """Interleaved timing of pa_trajectory_gn_step variants (assembler waves per trajectory,
-pa_debug_gn_set_assemblers) at 1000 x 24 and at the streaming pose stage's 3 x 24, HIP
+pa_debug_gn_set_assemblers; 128: the two-ended elimination, 64: cyclic reduction) at T x 24
+(default 1000 and the streaming pose stage's 3), HIP
 events over back-to-back launches; outputs checked against the shipped variant's.
 
-    python tools/gn_ab.py [--na 0 1 3 4] [--rounds 5]
+    python tools/gn_ab.py [--na 128 64 0] [--T 1000 3] [--rounds 5]
 """
 import argparse
 import os
@@ -15,7 +16,8 @@ sys.path.insert(0, ROOT)
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--na", type=int, nargs="+", default=[8, 0, 3])
+    p.add_argument("--na", type=int, nargs="+", default=[128, 64, 0])
+    p.add_argument("--T", type=int, nargs="+", default=[1000, 3])
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=20)
     a = p.parse_args()
@@ -26,7 +28,7 @@ def main():
     L_ = _lib.lib()
     dev = torch.device("cuda", 0)
     s = torch.cuda.current_stream(dev)
-    for T, L in ((1000, 24), (3, 24)):
+    for T, L in ((T, 24) for T in a.T):
         tr = synth.synthetic_trajectories(1, T, L)
         y = torch.as_tensor(tr["y"], device=dev)
         args, lin = pipeline.prepare_trajectories(y, tr["poses"], tr["vels"], tr["angvels"], tr["corners"], tr["K"],
@@ -90,6 +92,18 @@ def trace(T=3, L=24, variant=0):
     _lib.check(L_.pa_debug_gn_set_assemblers(0))
     s = buf.cpu().numpy().reshape(T, 256).astype(np.int64)
     t0 = s[0, 0]
+    if variant & 64:  # gn_cr_kernel's stamps (wave 0, 10 ns ticks)
+        ns = lambda j: (s[0, j] - t0) * 10  # noqa: E731
+        print(f"assembly (wave 0) {ns(2)} ns, barrier {ns(1)} ns")
+        for lv in range(6):
+            if s[0, 10 + 2 * lv]:
+                print(f"level {lv}: eliminated {ns(10 + 2 * lv)} ns, survivors {ns(11 + 2 * lv)} ns")
+        print(f"last solve {ns(30)} ns")
+        for lv in range(5, -1, -1):
+            if s[0, 31 + lv]:
+                print(f"back level {lv}: {ns(31 + lv)} ns")
+        print(f"end {ns(40)} ns")
+        return
     for l in range(L):
         a0, a1 = (s[0, 2 * l] - t0) * 10, (s[0, 2 * l + 1] - t0) * 10
         w, rd, sw, dn = ((s[0, 64 + 4 * l + j] - t0) * 10 for j in range(4))
