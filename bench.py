@@ -517,12 +517,28 @@ def factor_leg(dev, seed, rank, T=1000, L=24, reps=20):
     torch.cuda.synchronize(dev)
     t_gn = e0.elapsed_time(e1) / reps * 1e-3
     solved = int((plan.out["info"] == 0).sum())
+    # the streaming pose stage's size (3 cameras x 24 frames): the cyclic-reduction form
+    tr3 = synth.synthetic_trajectories(seed + 2 + rank, 3, L)
+    a3, out3 = pipeline.prepare_trajectories(torch.as_tensor(tr3["y"], device=dev), tr3["poses"], tr3["vels"],
+                                            tr3["angvels"], tr3["corners"], tr3["K"], T=3, L=L, dt=1 / 12,
+                                            proj_sigmas=[1.0, 1.0], dyn_sigmas=[0.1] * 6, cv_sigmas=[0.1] * 3)
+    pipeline.launch(a3, dev)
+    plan3 = pipeline.GNPlan(out3, T=3, L=L, lam=1e-3)
+    for _ in range(2):
+        plan3.launch()
+    e0.record(s)
+    for _ in range(reps):
+        plan3.launch()
+    e1.record(s)
+    torch.cuda.synchronize(dev)
+    t_gn3 = e0.elapsed_time(e1) / reps * 1e-3
     return {"workload": f"trajectory_linearize_{T}x{L}", "frames": F, "factors": n + 2 * m,
             "us_per_launch": round(t * 1e6, 2), "frames_per_s": round(F / t, 1), "factors_per_s": round((n + 2 * m) / t),
             "alg_bytes": bytes_in + bytes_out, "hbm_gbps": round((bytes_in + bytes_out) / t / 1e9, 1),
             "hbm_frac": round((bytes_in + bytes_out) / t / HBM_PEAK, 4), "dtype": "f64",
             "gn_step": {"us_per_step": round(t_gn * 1e6, 2), "trajectories": T, "solved": solved,
-                        "trajectories_per_s": round(T / t_gn, 1)}}
+                        "trajectories_per_s": round(T / t_gn, 1), "us_per_step_3x24": round(t_gn3 * 1e6, 2),
+                        "solved_3x24": int((plan3.out["info"] == 0).sum())}}
 
 
 def csrc_digest() -> str:

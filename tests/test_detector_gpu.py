@@ -344,6 +344,25 @@ def test_fp16x3_stride2_variants_agree_bit_for_bit(gold):
         assert np.abs(y - gold[f"{name}/y_ref_f32"]).max() * PX <= FP32_PX_MAX
 
 
+@pytest.mark.parametrize("B,small", [(64, False), (5, False), (3, True)])
+def test_fp16x3_stem_role_split_is_bit_identical(B, small):
+    """fp16x3 stem: the role-split kernel (shipped) against the all-waves form (variant 30):
+    the same products in the same order per accumulator, so the pooled (hi, lo) map and the
+    keypoints are bit for bit equal -- batched (16-row bands) and in the latency mode (2-row
+    bands)."""
+    m = model(0, precision="fp16x3")
+    if small:
+        m.set_split_k(8)
+    x = torch.from_numpy(synth.synthetic_frames(6, B)).cuda()
+    y0 = m(x)
+    try:
+        m.set_variants({0: 30})
+        y1 = m(x)
+    finally:
+        m.set_variants({})
+    assert torch.equal(y0, y1)
+
+
 def test_fp16x3_merged_steps_match_three_block_form(gold):
     """fp16x3 3x3 s1 convs: the merged x_hi steps (shipped: x_hi w_hi and x_hi w_lo from one
     fragment read) against three virtual blocks per 64 channels (variant 70).  The f32
