@@ -17,10 +17,43 @@
 
 namespace pa {
 
+// lo / hi = sum_s part[s][e .. e + 7], s in order 0 .. nsplit - 1 (NS > 0: nsplit == NS, all
+// loads issued first)
+template <int NS>
+__device__ __forceinline__ void splitk_sum(const float* __restrict__ part, int nsplit, unsigned n, unsigned e, f32x4& lo,
+                                           f32x4& hi) {
+  if constexpr (NS > 0) {
+    f32x4 pl[NS], ph[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      pl[s] = *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e);
+      ph[s] = *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e + 4);
+    }
+    lo = pl[0];
+    hi = ph[0];
+#pragma unroll
+    for (int s = 1; s < NS; ++s) {
+      lo += pl[s];
+      hi += ph[s];
+    }
+  } else {
+    lo = *reinterpret_cast<const f32x4*>(part + e);
+    hi = *reinterpret_cast<const f32x4*>(part + e + 4);
+    for (int s = 1; s < nsplit; ++s) {
+      lo += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e);
+      hi += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e + 4);
+    }
+  }
+}
+
 // out[p][c] = relu(sum_s part[s][p][c] + bias[c] (+ res[p][c])), 8 channels per thread,
 // splits summed in order 0 .. nsplit-1.  With out2 (a stride-2 entry's downsample), the
 // threads past n / 8 reduce the second partial set part[nsplit ..] into
 // out2[p][c] = sum_s + bias2[c] (no ReLU).
+// NS > 0: the split count at compile time -- every partial's loads are issued before the
+// first add (with a runtime count the loop waited out one memory latency per split: ~5 us
+// per launch at B = 3 whatever the split count); the sum order is the same.
+template <int NS>
 __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ part, int nsplit, unsigned n,
                                                      const float* __restrict__ bias, const _Float16* __restrict__ res,
                                                      _Float16* __restrict__ out, int Cout, const float* __restrict__ bias2,
@@ -36,11 +69,8 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ p
     res = nullptr;
   }
   const int c = (int)(e % (unsigned)Cout);
-  f32x4 lo = *reinterpret_cast<const f32x4*>(part + e), hi = *reinterpret_cast<const f32x4*>(part + e + 4);
-  for (int s = 1; s < nsplit; ++s) {
-    lo += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e);
-    hi += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e + 4);
-  }
+  f32x4 lo, hi;
+  splitk_sum<NS>(part, nsplit, n, e, lo, hi);
   // the batched epilogue's order: (acc + bias) (+ res), then ReLU
   lo += *reinterpret_cast<const f32x4*>(bias + c);
   hi += *reinterpret_cast<const f32x4*>(bias + c + 4);
@@ -64,8 +94,13 @@ static int launch_reduce(const float* part, int nsplit, size_t n, const float* b
                          int Cout, const float* bias2, _Float16* out2, hipStream_t s) {
   PA_CHECK(n % 8 == 0 && n < 0x40000000u && Cout % 8 == 0, "split-K reduce: %zu elements", n);
   const size_t threads = (out2 ? 2 * n : n) / 8;
-  hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, part, nsplit, (unsigned)n, bias,
-                     res, out, Cout, bias2, out2);
+  const dim3 g((unsigned)((threads + 255) / 256));
+  switch (g_variant[7] == 5 ? 0 : nsplit) {  // (variant 7:5: the runtime-count loop, A/B)
+    case 2: hipLaunchKernelGGL(splitk_reduce<2>, g, dim3(256), 0, s, part, nsplit, (unsigned)n, bias, res, out, Cout, bias2, out2); break;
+    case 4: hipLaunchKernelGGL(splitk_reduce<4>, g, dim3(256), 0, s, part, nsplit, (unsigned)n, bias, res, out, Cout, bias2, out2); break;
+    case 8: hipLaunchKernelGGL(splitk_reduce<8>, g, dim3(256), 0, s, part, nsplit, (unsigned)n, bias, res, out, Cout, bias2, out2); break;
+    default: hipLaunchKernelGGL(splitk_reduce<0>, g, dim3(256), 0, s, part, nsplit, (unsigned)n, bias, res, out, Cout, bias2, out2);
+  }
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -113,6 +148,7 @@ int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s, bool split_l2) {
 // split-order sum (the partials carry the weights' 2^e; the unscale is exact).  out / res
 // are [pixel][hi (Cout) | lo (Cout)]; with out2 (stride-2 entry) the second partial set is
 // the downsample: sum * scale2 + bias2, no ReLU.
+template <int NS>
 __global__ __launch_bounds__(256) void splitk_reduce_x3(const float* __restrict__ part, int nsplit, unsigned n,
                                                         const float* __restrict__ bias, const float* __restrict__ scale,
                                                         const _Float16* __restrict__ res, _Float16* __restrict__ out,
@@ -131,11 +167,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_x3(const float* __restrict_
   }
   const unsigned pix = e / (unsigned)Cout;
   const int c = (int)(e - pix * (unsigned)Cout);
-  f32x4 lo = *reinterpret_cast<const f32x4*>(part + e), hi = *reinterpret_cast<const f32x4*>(part + e + 4);
-  for (int s = 1; s < nsplit; ++s) {
-    lo += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e);
-    hi += *reinterpret_cast<const f32x4*>(part + (size_t)s * n + e + 4);
-  }
+  f32x4 lo, hi;
+  splitk_sum<NS>(part, nsplit, n, e, lo, hi);
   const f32x4 b0 = *reinterpret_cast<const f32x4*>(bias + c), b1 = *reinterpret_cast<const f32x4*>(bias + c + 4);
   const f32x4 s0 = *reinterpret_cast<const f32x4*>(scale + c), s1 = *reinterpret_cast<const f32x4*>(scale + c + 4);
   const size_t o = (size_t)pix * 2 * Cout + c;
@@ -163,8 +196,13 @@ static int launch_reduce_x3(const float* part, int nsplit, size_t n, const float
   PA_CHECK(n % 8 == 0 && n < 0x40000000u && Cout % 8 == 0 && scale && (!out2 || scale2),
            "split-K reduce (fp16x3): %zu elements", n);
   const size_t threads = (out2 ? 2 * n : n) / 8;
-  hipLaunchKernelGGL(splitk_reduce_x3, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, part, nsplit,
-                     (unsigned)n, bias, scale, res, out, Cout, bias2, scale2, out2);
+  const dim3 g((unsigned)((threads + 255) / 256));
+  switch (g_variant[7] == 5 ? 0 : nsplit) {
+    case 2: hipLaunchKernelGGL(splitk_reduce_x3<2>, g, dim3(256), 0, s, part, nsplit, (unsigned)n, bias, scale, res, out, Cout, bias2, scale2, out2); break;
+    case 4: hipLaunchKernelGGL(splitk_reduce_x3<4>, g, dim3(256), 0, s, part, nsplit, (unsigned)n, bias, scale, res, out, Cout, bias2, scale2, out2); break;
+    case 8: hipLaunchKernelGGL(splitk_reduce_x3<8>, g, dim3(256), 0, s, part, nsplit, (unsigned)n, bias, scale, res, out, Cout, bias2, scale2, out2); break;
+    default: hipLaunchKernelGGL(splitk_reduce_x3<0>, g, dim3(256), 0, s, part, nsplit, (unsigned)n, bias, scale, res, out, Cout, bias2, scale2, out2);
+  }
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

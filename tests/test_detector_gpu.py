@@ -363,6 +363,22 @@ def test_fp16x3_stem_role_split_is_bit_identical(B, small):
     assert torch.equal(y0, y1)
 
 
+@pytest.mark.parametrize("precision", ["fp16", "fp16x3"])
+def test_split_k_reduce_forms_bit_identical(precision):
+    """The split-K reduces with the split count at compile time (every partial loaded before
+    the first add) against the runtime-count loop (variant 7:5): same sum order, same bits."""
+    m = model(0, precision=precision)
+    m.set_split_k(8)
+    x = torch.from_numpy(synth.synthetic_frames(8, 3)).cuda()
+    y0 = m(x)
+    try:
+        m.set_variants({7: 5})
+        y1 = m(x)
+    finally:
+        m.set_variants({})
+    assert torch.equal(y0, y1)
+
+
 def test_fp16x3_merged_steps_match_three_block_form(gold):
     """fp16x3 3x3 s1 convs: the merged x_hi steps (shipped: x_hi w_hi and x_hi w_lo from one
     fragment read) against three virtual blocks per 64 channels (variant 70).  The f32

@@ -23,6 +23,7 @@ def main():
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--precision", default="fp16")
     p.add_argument("--reps", type=int, default=10)
+    p.add_argument("--split-k", type=int, default=0, help="latency mode max batch (pa_detector_set_split_k)")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -33,6 +34,8 @@ def main():
     L = _lib.lib()
     m = KeypointCNN(num_channels=4, precision=a.precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
+    if a.split_k:
+        m.set_split_k(a.split_k)
     x = torch.from_numpy(synth.synthetic_frames(0, a.batch)).cuda()
     ref = None
     res = {}
