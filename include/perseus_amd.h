@@ -251,6 +251,16 @@ int pa_window_retract(int T, int L, const double* delta_dev, const int32_t* info
 int pa_window_retract_newest(int T, int L, const double* delta_dev, const int32_t* info_dev, double* pose_dev,
                              double* angvel_dev, double* vel_dev, double* newest_pose_dev, void* stream);
 
+/* One streaming tick's pose stage (config 4) in two launches, bit for bit the sequence
+ * pa_window_advance_n(y_new) -> pa_trajectory_linearize(args) -> pa_trajectory_gn_step
+ * (lambda; delta, info; D / E / g not written) -> pa_window_retract_newest(newest_pose).
+ * args: the window's pa_traj_args (args->y / pose / vel / angvel ARE the window arrays,
+ * advanced and retracted in place; nvalid required; every factor output and Jacobian
+ * required, whitening as the caller wants it for the GN step).  T <= the device's CU count,
+ * 2 <= L <= 24, n_kp <= 16 (PA_EINVAL otherwise: use the four calls). */
+int pa_window_pose_tick(const pa_traj_args* args, const float* y_new_dev, double lambda, double* delta_dev,
+                        int32_t* info_dev, double* newest_pose_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,6 +73,8 @@ _SIGS = {
     "pa_debug_gn_set_assemblers": (C.c_int, [C.c_int]),
     "pa_window_retract_newest": (C.c_int, [C.c_int, C.c_int] + [C.c_void_p] * 7),
     "pa_debug_gn_set_trace": (C.c_int, [C.c_void_p]),
+    "pa_window_pose_tick": (C.c_int, [C.POINTER(TrajArgs), C.c_void_p, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p]),
     "pa_loss_statistics_workspace": (C.c_size_t, [C.c_longlong]),
     "pa_loss_statistics": (C.c_int, [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "pa_proj_linearize": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,

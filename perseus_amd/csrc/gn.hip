@@ -22,6 +22,7 @@
 // f64 throughout.
 // Jacobians are column-major per factor (include/perseus_amd.h).
 #include "common.h"
+#include "factors_dev.h"
 
 namespace pa {
 
@@ -1110,8 +1111,25 @@ __device__ __forceinline__ void gn_mm_store(double* out, const gn_d4& c, double 
     for (int v = 0; v < 3; ++v) out[(lk + 4 * v) * NV + li] = s * c[v];
 }
 
+// LDS of gn_cr_run: fb (S | C | b per frame) and the pool (assembly staging, then the level data)
 template <int RP, int NS>
-__global__ __launch_bounds__(64 * GN_CR_W, 1) void gn_cr_kernel(GnArgs a) {
+struct GnCrLds {
+  static constexpr int BLK = 2 * gn::NB + gn::NV;
+  static constexpr int LM = GN_CR_LMAX, W = GN_CR_W;
+  static constexpr int CHD = (int)(sizeof(GnChainLds) / sizeof(double));
+  static constexpr int STGD = (int)(sizeof(GnStage<RP>) / sizeof(double));
+  static constexpr int FR = 2 * gn::NB + gn::NV;
+  static constexpr bool PAIR = NS == W && 2 * W >= LM;
+  static constexpr int SLAB0 = 2 * FR + CHD > STGD ? 2 * FR + CHD : STGD;
+  static constexpr int SLAB = (SLAB0 + 1) / 2 * 2;
+  static constexpr int POST = LM * FR + W * CHD;
+  static constexpr int STG = NS * STGD;
+  static constexpr int POOL = PAIR ? W * SLAB : (POST > STG ? POST : STG);
+};
+
+// trajectory t on this workgroup (64 * GN_CR_W threads); fb / pool: GnCrLds<RP, NS> in LDS
+template <int RP, int NS>
+__device__ __forceinline__ void gn_cr_run(const GnArgs& a, int t, double (*fb)[2 * gn::NB + gn::NV], double* pool) {
   using namespace gn;
   constexpr int BLK = 2 * NB + NV;
   constexpr int LM = GN_CR_LMAX, W = GN_CR_W;
@@ -1131,12 +1149,10 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void gn_cr_kernel(GnArgs a) {
   constexpr int POOL = PAIR ? W * SLAB : (POST > STG ? POST : STG);
   constexpr int NOFAIL = 0x7fffffff;
   static_assert(NS <= W, "assembler waves");
-  __shared__ __attribute__((aligned(16))) double fb[LM][BLK];  // S | C | b per frame (delta over S at the end)
-  __shared__ __attribute__((aligned(16))) double pool[POOL];   // assembly staging, then the level data
-  __shared__ signed char lst[8][LM];                           // active frames per level
+  static_assert(POOL == GnCrLds<RP, NS>::POOL && BLK == GnCrLds<RP, NS>::BLK, "LDS layout");
+  __shared__ signed char lst[8][LM];  // active frames per level
   __shared__ int lcnt[8], lpe[8];
   __shared__ int nlev_s, fail;
-  const int t = blockIdx.x;
   const int wv = threadIdx.x >> 6;
   const int i = threadIdx.x & 63;
   const int L = a.L;
@@ -1163,6 +1179,10 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void gn_cr_kernel(GnArgs a) {
     nlev_s = lv;
     fail = NOFAIL;
   }
+  // the level lists and `fail` are in place before any wave eliminates or reads them (LDS
+  // holds whatever the previous kernel left: an unsynchronised read of nlev_s gave waves
+  // different level counts, i.e. different barrier counts -- a hang)
+  __syncthreads();
   if (wv == 0) gn_stamp(a, t, 0);
   const bool act = i < 36;
   const int ii = act ? i : 35;
@@ -1226,8 +1246,8 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void gn_cr_kernel(GnArgs a) {
     __syncthreads();
     for (int l = wv; l < L; l += W) init(l);
   }
-  const int nlev = nlev_s;
   __syncthreads();
+  const int nlev = nlev_s;  // (after a barrier: thread 0 wrote it)
   if (wv == 0) gn_stamp(a, t, 1);
   int lv = 0;
   for (; lv < nlev; ++lv) {
@@ -1327,6 +1347,85 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void gn_cr_kernel(GnArgs a) {
   if (wv == 0) gn_stamp(a, t, 40);
 }
 
+template <int RP, int NS>
+__global__ __launch_bounds__(64 * GN_CR_W, 1) void gn_cr_kernel(GnArgs a) {
+  using Ld = GnCrLds<RP, NS>;
+  __shared__ __attribute__((aligned(16))) double fb[Ld::LM][Ld::BLK];
+  __shared__ __attribute__((aligned(16))) double pool[Ld::POOL];
+  gn_cr_run<RP, NS>(a, blockIdx.x, fb, pool);
+}
+
+// ---------------------------------------------------------------- the streaming pose tick, fused
+// pa_window_pose_tick: one tick's pose stage (config 4) as two launches instead of four, one
+// workgroup per trajectory (camera) in each:
+//   pose_tick_lin_kernel (6 waves)  advance: window_advance_body (the window shifts, y_new
+//        lands, frame L-1 predicted); linearize: the trajectory's factors as a T = 1 view --
+//        waves 0-1 its L-1 dynamics factors (traj_dyn_block), then one wave per 256
+//        projection factors and one for the constant-velocity ones (traj_unit_wave)
+//   pose_tick_gn_kernel (12 waves)  the GN step (gn_cr_run, block cyclic reduction), then the
+//        retract (window_retract_one per frame, the newest pose to `newest`)
+// (One 12-wave launch for all four would hold the dynamics factors' ~220 VGPRs at three waves
+// per SIMD: 240 spilled.)  Every phase is its separate kernel's device code, so the window,
+// the factors, delta, info and the newest poses are bit for bit the four-launch sequence's
+// (tests/test_streaming_pose_gpu.py).
+constexpr int TICK_LIN_W = 6;
+__global__ __launch_bounds__(64 * TICK_LIN_W) void pose_tick_lin_kernel(pa_traj_args ta, const float* __restrict__ y_new) {
+  static_assert((trj::STAGE + 4 * trj::UNIT) * 8 <= 96 * 1024, "factor staging");
+  __shared__ __attribute__((aligned(16))) double st[trj::STAGE + 4 * trj::UNIT];
+  const int t = blockIdx.x, L = ta.L, K = ta.n_kp, wv = threadIdx.x >> 6;
+  window_advance_body(t, threadIdx.x, 64 * TICK_LIN_W, L, K, y_new, const_cast<float*>(ta.y),
+                      const_cast<double*>(ta.pose), const_cast<double*>(ta.angvel), const_cast<double*>(ta.vel), ta.dt,
+                      ta.vel_frame, const_cast<int32_t*>(ta.nvalid));
+  __syncthreads();
+  // trajectory t's factors: the arrays of a T = 1 problem start at its records
+  pa_traj_args a1 = ta;
+  {
+    const long f0 = (long)t * L, p0 = f0 * K, d0 = (long)t * (L - 1);
+    auto off = [](auto* q, long n) { return q ? q + n : q; };
+    a1.T = 1;
+    a1.y = ta.y + f0 * 2 * K;
+    a1.pose = ta.pose + f0 * 12;
+    a1.vel = ta.vel + f0 * 3;
+    a1.angvel = ta.angvel + f0 * 3;
+    a1.r_proj = off(ta.r_proj, p0 * 2);
+    a1.j_proj = off(ta.j_proj, p0 * 12);
+    a1.err_proj = off(ta.err_proj, p0);
+    a1.status = off(ta.status, p0);
+    a1.r_dyn = off(ta.r_dyn, d0 * 6);
+    a1.j_dyn0 = off(ta.j_dyn0, d0 * 36);
+    a1.j_dyn1 = off(ta.j_dyn1, d0 * 18);
+    a1.j_dyn2 = off(ta.j_dyn2, d0 * 18);
+    a1.j_dyn3 = off(ta.j_dyn3, d0 * 36);
+    a1.err_dyn = off(ta.err_dyn, d0);
+    a1.r_cv = off(ta.r_cv, d0 * 3);
+    a1.j_cv0 = off(ta.j_cv0, d0 * 9);
+    a1.j_cv1 = off(ta.j_cv1, d0 * 9);
+    a1.err_cv = off(ta.err_cv, d0);
+    a1.nvalid = off(ta.nvalid, (long)t);
+  }
+  const int wp = (L * K + 64 * trj::PPW - 1) / (64 * trj::PPW);  // projection units (<= 2); unit wp: constant velocity
+  if (wv < 2) {
+    traj_dyn_block(a1, 0, st, nullptr);  // (its one LDS barrier is matched by every other wave's below)
+  } else {
+    if (wv - 2 <= wp) traj_unit_wave(a1, wv - 2, st + trj::STAGE + (wv - 2) * trj::UNIT, nullptr);
+    lds_barrier();
+  }
+}
+
+template <int RP>
+__global__ __launch_bounds__(64 * GN_CR_W, 1) void pose_tick_gn_kernel(GnArgs g, double* pose, double* angvel,
+                                                                        double* vel, double* newest) {
+  constexpr int NS = RP <= 34 ? 12 : 8;
+  using Ld = GnCrLds<RP, NS>;
+  __shared__ __attribute__((aligned(16))) double fb[Ld::LM][Ld::BLK];
+  __shared__ __attribute__((aligned(16))) double pool[Ld::POOL];
+  const int t = blockIdx.x, L = g.L;
+  gn_cr_run<RP, NS>(g, t, fb, pool);
+  __syncthreads();
+  if ((int)threadIdx.x < L)
+    window_retract_one((long)t * L + threadIdx.x, L, g.delta, g.info, pose, angvel, vel, newest);
+}
+
 // assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * legacy;
 // 0 = the shipped choice)
 static int g_gn_na = 0;
@@ -1357,6 +1456,7 @@ static void launch_gn_sv(const GnArgs& a, int na, hipStream_t s) {
 // cyclic reduction for launches of few trajectories (v & 64 forces it, v & 128 never)
 template <int RP>
 static void launch_gn(const GnArgs& a, int v, hipStream_t s) {
+  v &= 255;
   const bool cr_ok = a.L <= GN_CR_LMAX && !(v & 63);
   // (T x 24, us, two-ended / cyclic: 3: 41.3 / 33.4, 64: 41.9 / 33.9, 256: 42.6 / 34.4,
   // 512: 54.1 / 66.6, 1000: 71.3 / 130.8; profiles/r04i/gn_cr_ab.log)
@@ -1382,11 +1482,44 @@ int pa_debug_gn_set_trace(unsigned long long* trace_dev) {
 }
 
 int pa_debug_gn_set_assemblers(int na) {
-  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 256 && !((na & 8) && (na & 16)) && !((na & 64) && (na & 128)),
+  PA_CHECK((na & 7) <= 4 && na >= 0 && na < 4096 && !((na & 8) && (na & 16)) && !((na & 64) && (na & 128)),
            "gn variant %d: assembler waves (0..4) + 8 * legacy Cholesky or 16 * single-chain solver, 32: "
            "two-ended kernel in its 4-per-CU form, 64: cyclic reduction (L <= 24), 128: never cyclic "
            "reduction", na);
   pa::g_gn_na = na;
+  return PA_OK;
+}
+
+int pa_window_pose_tick(const pa_traj_args* ta, const float* y_new, double lambda, double* delta, int32_t* info,
+                        double* newest_pose, void* stream) {
+  PA_CHECK(ta && y_new && delta && info, "pose tick: null args / y_new / delta / info");
+  const int T = ta->T, L = ta->L, K = ta->n_kp;
+  PA_CHECK(T >= 0 && T <= pa::g_gn_cus() && L >= 2 && L <= pa::GN_CR_LMAX && K >= 0 && K <= pa::GN_KMAX,
+           "pose tick: T %d (<= %d CUs), L %d (2..%d), n_kp %d (<= %d)", T, pa::g_gn_cus(), L, pa::GN_CR_LMAX, K,
+           pa::GN_KMAX);
+  if (T == 0) return PA_OK;
+  PA_CHECK(lambda >= 0.0, "pose tick: lambda %g < 0", lambda);
+  PA_CHECK(ta->y && ta->pose && ta->vel && ta->angvel && ta->corners && ta->K && ta->nvalid,
+           "pose tick: null window / model pointer");
+  PA_CHECK((K == 0 || (ta->r_proj && ta->j_proj && ta->status)) && ta->r_dyn && ta->j_dyn0 && ta->j_dyn1 &&
+               ta->j_dyn2 && ta->j_dyn3 && ta->r_cv && ta->j_cv0 && ta->j_cv1,
+           "pose tick: the factor outputs and every Jacobian are required");
+  const pa::GnArgs g{T,     L,     K,     ta->r_proj, ta->j_proj, ta->status, ta->r_dyn, ta->j_dyn0,
+                     ta->j_dyn1, ta->j_dyn2, ta->j_dyn3, ta->r_cv, ta->j_cv0, ta->j_cv1, lambda, nullptr,
+                     nullptr, nullptr, delta, info, nullptr, nullptr};
+  const hipStream_t s = (hipStream_t)stream;
+  if (!(pa::g_gn_na & 2048)) hipLaunchKernelGGL(pa::pose_tick_lin_kernel, dim3(T), dim3(64 * pa::TICK_LIN_W), 0, s, *ta, y_new);
+  if (pa::g_gn_na & 1024) { PA_LAUNCH_CHECK(); return PA_OK; }
+  double* pose = const_cast<double*>(ta->pose);
+  double* angvel = const_cast<double*>(ta->angvel);
+  double* vel = const_cast<double*>(ta->vel);
+  if (K == 8)
+    hipLaunchKernelGGL(pa::pose_tick_gn_kernel<34>, dim3(T), dim3(64 * pa::GN_CR_W), 0, s, g, pose, angvel, vel,
+                       newest_pose);
+  else
+    hipLaunchKernelGGL(pa::pose_tick_gn_kernel<2 * pa::GN_KMAX + 18>, dim3(T), dim3(64 * pa::GN_CR_W), 0, s, g, pose,
+                       angvel, vel, newest_pose);
+  PA_LAUNCH_CHECK();
   return PA_OK;
 }
 

@@ -209,6 +209,22 @@ def window_advance(y_new: torch.Tensor, win: dict, *, dt: float, vel_frame: str 
             _lib.VEL_WORLD if vel_frame == "world" else _lib.VEL_BODY, _lib.stream_of(dev)), "pa_window_advance")
 
 
+TICK_MAX_L = 24  # pa_window_pose_tick: L <= 24 (the cyclic-reduction GN step), T <= the CU count
+
+
+def window_pose_tick(args, y_new: torch.Tensor, *, lam: float, delta: torch.Tensor, info: torch.Tensor,
+                     newest: torch.Tensor | None = None) -> None:
+    """pa_window_pose_tick on the device's current stream: window_advance(y_new) ->
+    pa_trajectory_linearize(args) -> pa_trajectory_gn_step (delta, info) ->
+    window_retract(newest) in two launches, bit for bit that sequence.  `args` comes from
+    prepare_trajectories over the window arrays (with nvalid, whitening sigmas and Jacobians)."""
+    dev = y_new.device
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pa_window_pose_tick(C.byref(args), y_new.data_ptr(), float(lam), delta.data_ptr(),
+                                                  info.data_ptr(), _lib.ptr(newest), _lib.stream_of(dev)),
+                   "pa_window_pose_tick")
+
+
 def window_retract(win: dict, delta: torch.Tensor, info: torch.Tensor | None = None,
                    newest: torch.Tensor | None = None) -> None:
     """pa_window_retract on the device's current stream: pose <- pose Exp(delta[:6]),

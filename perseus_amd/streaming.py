@@ -142,7 +142,13 @@ class StreamingPipeline:
         self.out_h.copy_(self.out_d, non_blocking=True)  # pixels (+ info, newest poses): one D2H
 
     def _enqueue_pose(self):
-        """The pose stage on the current stream, from the keypoints in self.y (HBM-resident window)."""
+        """The pose stage on the current stream, from the keypoints in self.y (HBM-resident window):
+        advance -> linearize -> GN step -> retract, as pa_window_pose_tick's two launches
+        (fused) or the four separate ones (bit-identical; windows above 24 frames)."""
+        if self.fused_pose:
+            pipeline.window_pose_tick(self.traj_args, self.y, lam=self.gn.lam, delta=self.gn.out["delta"],
+                                      info=self.gn.out["info"], newest=self.pose_d)
+            return
         pipeline.window_advance(self.y, self.win, dt=self.dt, vel_frame=self.vel_frame, nvalid=self.nvalid)
         pipeline.launch(self.traj_args, self.dev)
         self.gn.launch()  # delta, and info straight into the output block
@@ -180,6 +186,7 @@ class StreamingPipeline:
             assert self.lin["_keep"][("y", "pose", "vel", "angvel").index(k)].data_ptr() == self.win[k].data_ptr()
         self.gn = pipeline.GNPlan(self.lin, T=n, L=Lw, lam=lam)
         self.gn.out["info"] = self.info_d  # the GN step writes info into the output block
+        self.fused_pose = Lw <= pipeline.TICK_MAX_L and n <= 256
 
     def reset_window(self) -> None:
         """Every frame of every camera's window back to the initial state (keypoints 0, no
@@ -196,6 +203,7 @@ class StreamingPipeline:
         """Host copies of the window (y, pose, vel, angvel) after the last tick."""
         self.stream.synchronize()
         return {k: v.cpu().numpy().copy() for k, v in self.win.items()}
+
     def stage(self, rgb: np.ndarray, depth: np.ndarray) -> None:
         """Copy one tick of camera frames (n, Hs, Ws, 3) uint8 + (n, Hs, Ws) f32 metres
         into the pinned staging buffers (centre crop only when host_crop)."""

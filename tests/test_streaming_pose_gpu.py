@@ -14,7 +14,9 @@ trajectory linearize (the reference's three factors, perseus/smoother/factors.py
     against the same oracle chain;
   * the smoother tracks a pose: 40 ticks of exact keypoints of a known cube trajectory that
     follows the dynamics model, info == 0 on every tick, and the newest pose converges to the
-    true one.
+    true one;
+  * the fused pose tick (pa_window_pose_tick, the default for windows <= 24 frames) equals the
+    four separate launches bit for bit.
 """
 import numpy as np
 import pytest
@@ -124,6 +126,32 @@ def test_pose_graph_matches_eager(precision):
     np.testing.assert_array_equal(ig, ie)
     g.close()
     e.close()
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_fused_pose_tick_matches_four_launches(model, graph):
+    """pa_window_pose_tick (advance + linearize, then GN step + retract: two launches, the
+    shipped tick for windows <= 24 frames) against the four separate launches, bit for bit:
+    poses, info, the window, every factor output and delta, over ticks that fill the window."""
+    f, s = _pipe(model, graph), _pipe(model, graph)
+    assert f.fused_pose
+    s.fused_pose = False
+    truth, _, _ = _truth(3, LW + 3)
+    rng = np.random.default_rng(11)
+    for k in range(LW + 3):
+        y = _keypoints(truth[k], 0.5, rng)
+        qf, inf_ = f.tick_keypoints(y)
+        qs, ins = s.tick_keypoints(y)
+        np.testing.assert_array_equal(qf, qs)
+        np.testing.assert_array_equal(inf_, ins)
+        for key, v in f.window_state().items():
+            np.testing.assert_array_equal(v, s.window_state()[key], err_msg=key)
+        for key, v in f.lin.items():
+            if isinstance(v, torch.Tensor):
+                assert torch.equal(v, s.lin[key]), key
+        assert torch.equal(f.gn.out["delta"], s.gn.out["delta"])
+    f.close()
+    s.close()
 
 
 def _whiten(ref):
