@@ -326,7 +326,8 @@ def trajset_leg(model, x, args, dev, world, rank, reps=3):
             "timing": f"wall clock, barrier + synchronize, max over ranks, median of {reps}"}
 
 
-def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pose", "pose_parity", "pixels")):
+def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pose", "pose_parity", "pixels"),
+                  zero_copy=None):
     """configs[4]: 3 x 720p RGBD cameras paced at `hz`, one StreamingPipeline tick per
     camera period (pinned host staging of the centre crops, one hipGraph replay: H2D,
     fused-preprocess forward at B = cams, denormalize, D2H pixels; mode "pose" adds the
@@ -356,7 +357,7 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pos
     for mode in modes:
         kw = dict(pose_window=window, proj_sigma=40.0) if mode.startswith("pose") else {}
         pipe = StreamingPipeline(parity if mode == "pose_parity" else model, n_cams=cams, graph=True, host_crop=True,
-                                 device=dev, **kw)
+                                 device=dev, zero_copy=zero_copy, **kw)
         for i in range(10):
             pipe(rgbs[i % n_src], deps[i % n_src])
         n = ticks if mode.startswith("pose") else max(ticks // 3, 30)

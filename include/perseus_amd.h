@@ -96,6 +96,10 @@ int pa_detector_forward_rgbd(pa_detector* d, const uint8_t* rgb_dev, const float
  * tick's detector call (one launch fewer per tick). */
 int pa_detector_forward_rgbd_px(pa_detector* d, const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws,
                                 int bgr, float near_m, float far_m, float* y_dev, float* px_dev, void* stream);
+/* The device address of a mapped pinned host buffer (hipHostGetDevicePointer): forward_rgbd
+ * may read the camera frames straight from host memory over PCIe (zero-copy), so a tick
+ * needs no H2D copy before the stem (StreamingPipeline(zero_copy=True)). */
+int pa_host_device_pointer(const void* host, void** dev);
 
 /* Same forward with a HIP event after every kernel: writes up to max_n per-kernel
  * durations (ms) into ms_out and their names into names_out (may be NULL), returns

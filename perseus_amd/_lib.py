@@ -73,6 +73,7 @@ _SIGS = {
     "pa_debug_gn_set_assemblers": (C.c_int, [C.c_int]),
     "pa_window_retract_newest": (C.c_int, [C.c_int, C.c_int] + [C.c_void_p] * 7),
     "pa_debug_gn_set_trace": (C.c_int, [C.c_void_p]),
+    "pa_host_device_pointer": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "pa_window_pose_tick": (C.c_int, [C.POINTER(TrajArgs), C.c_void_p, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p]),
     "pa_loss_statistics_workspace": (C.c_size_t, [C.c_longlong]),

@@ -695,6 +695,15 @@ int pa_detector_forward_rgbd_px(pa_detector* d, const uint8_t* rgb_dev, const fl
   return pa::forward_rgbd(d, src, B, y_dev, (hipStream_t)stream, px_dev);
 }
 
+int pa_host_device_pointer(const void* host, void** dev) {
+  PA_CHECK(host && dev, "host_device_pointer: null pointer");
+  void* p = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&p, const_cast<void*>(host), 0);
+  PA_CHECK(e == hipSuccess && p, "hipHostGetDevicePointer: %s (not a mapped pinned host buffer?)", hipGetErrorString(e));
+  *dev = p;
+  return PA_OK;
+}
+
 const char* pa_last_error(void) { return pa::g_err.c_str(); }
 const char* pa_version(void) { return "perseus_amd 0.1 gfx950"; }
 

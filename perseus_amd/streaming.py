@@ -32,6 +32,8 @@ allocated before capture so no allocation happens inside the graph.
 
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import torch
 
@@ -50,7 +52,8 @@ class StreamingPipeline:
                  graph: bool = True, near: float | None = None, far: float | None = None, device=None,
                  pose_window: int = 0, K=None, corners=None, dt: float = 1.0 / 30.0, vel_frame: str = "world",
                  proj_sigma: float = 1.0, dyn_sigma: float = 0.1, cv_sigma: float = 0.1, lam: float = 1e-2,
-                 init_pose=None, init_vel=None, init_angvel=None, split_k: bool = True):
+                 init_pose=None, init_vel=None, init_angvel=None, split_k: bool = True,
+                 zero_copy: bool | None = None):
         if not torch.cuda.is_available():
             raise RuntimeError("StreamingPipeline needs a ROCm GPU (no CPU fallback)")
         cam_K = K  # (the name K is the keypoint count below)
@@ -92,6 +95,17 @@ class StreamingPipeline:
 
         self.rgb_h, self.depth_h, self.px_h, self.info_h, self.pose_h = views(self.in_h, self.out_h)
         self.rgb_d, self.depth_d, self.px_d, self.info_d, self.pose_d = views(self.in_d, self.out_d)
+        # zero_copy: the stem (fp16) / the preprocess kernel (fp16x3, fp32) read the pinned staging
+        # over PCIe, no H2D copy in the tick.  None: on for the preprocess-kernel precisions (its
+        # coalesced reads beat the copy: fp16x3 pose tick 0.330 -> 0.322 ms device), off for fp16
+        # (the stem's row loads over PCIe lose: 0.252 -> 0.267 ms; profiles/r04v/)
+        self.zero_copy = (model.precision != "fp16") if zero_copy is None else bool(zero_copy)
+        self._src = (self.rgb_d.data_ptr(), self.depth_d.data_ptr())
+        if self.zero_copy:
+            dp = C.c_void_p()
+            _lib.check(_lib.lib().pa_host_device_pointer(C.c_void_p(self.in_h.data_ptr()), C.byref(dp)),
+                       "host_device_pointer")
+            self._src = (dp.value, dp.value + nr)
         self.y = torch.empty((n, 2 * K), dtype=torch.float32, device=self.dev)
         self.y_h = torch.empty((n, 2 * K), dtype=torch.float32).pin_memory()  # tick_keypoints' input
         self.pose_graph = None
@@ -131,10 +145,11 @@ class StreamingPipeline:
         """H2D, preprocess + forward + denormalize, [pose stage], D2H on the current stream."""
         L = _lib.lib()
         s = torch.cuda.current_stream(self.dev).cuda_stream
-        self.in_d.copy_(self.in_h, non_blocking=True)
+        if not self.zero_copy:
+            self.in_d.copy_(self.in_h, non_blocking=True)
         # fp16: the preprocess runs inside the stem's row loads (SURVEY 8f.1); fp16x3 / fp32: the
         # preprocess kernel into the handle's staging, then the forward; the denormalize in the head
-        _lib.check(L.pa_detector_forward_rgbd_px(self._h, self.rgb_d.data_ptr(), self.depth_d.data_ptr(), self.n,
+        _lib.check(L.pa_detector_forward_rgbd_px(self._h, self._src[0], self._src[1], self.n,
                                                  self.sh, self.sw, int(self.bgr), self.near, self.far,
                                                  self.y.data_ptr(), self.px_d.data_ptr(), s), "forward_rgbd_px")
         if self.pose_L:

@@ -135,3 +135,26 @@ def test_parity_grade_tick_fp16x3(model_x3, n):
     err = np.abs(out.astype(np.float64) - px64).max()
     print(f"fp16x3 tick, {n} camera(s): max |px - px_f64| = {err:.3e}")
     assert err <= 1e-3
+
+
+@pytest.mark.parametrize("precision", ["fp16", "fp16x3"])
+def test_zero_copy_tick_matches_copying_tick(model, model_x3, precision):
+    """zero_copy (the stem / preprocess kernel read the pinned staging over PCIe, no H2D
+    copy; the default for fp16x3) against the copying tick: pixels bit for bit, graph and
+    eager, with the pose stage."""
+    m = model if precision == "fp16" else model_x3
+    a = StreamingPipeline(m, n_cams=3, graph=True, zero_copy=False, pose_window=6)
+    b = StreamingPipeline(m, n_cams=3, graph=True, zero_copy=True, pose_window=6)
+    c = StreamingPipeline(m, n_cams=3, graph=False, zero_copy=True, pose_window=6)
+    assert b.zero_copy and not a.zero_copy
+    dflt = StreamingPipeline(m, n_cams=1)
+    assert dflt.zero_copy == (precision != "fp16")
+    dflt.close()
+    for seed in range(3):
+        rgb, d = _frames(40 + seed, 3)
+        ra, rb, rc = a.tick(rgb, d), b.tick(rgb, d), c.tick(rgb, d)
+        for x, y, z in zip(ra, rb, rc):
+            np.testing.assert_array_equal(x, y)
+            np.testing.assert_array_equal(x, z)
+    for p in (a, b, c):
+        p.close()

@@ -23,6 +23,7 @@ def main():
     p.add_argument("--hz", type=float, default=30.0)
     p.add_argument("--cams", type=int, default=3)
     p.add_argument("--window", type=int, default=24)
+    p.add_argument("--zero-copy", type=int, default=None, help="1 / 0: the tick reads the pinned staging (no H2D copy); default per precision")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -34,7 +35,7 @@ def main():
     m = KeypointCNN(num_channels=4)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
     dev = torch.device("cuda", 0)
-    print(json.dumps(streaming_leg(m, dev, a.ticks, a.hz, a.cams, a.window)))
+    print(json.dumps(streaming_leg(m, dev, a.ticks, a.hz, a.cams, a.window, zero_copy=None if a.zero_copy is None else bool(a.zero_copy))))
 
 
 if __name__ == "__main__":
