@@ -286,3 +286,21 @@ def test_pose_window_rejects_bad_config(model):
         StreamingPipeline(model, pose_window=1)
     with pytest.raises(AssertionError):
         StreamingPipeline(model, pose_window=4, vel_frame="camera")
+
+
+def test_fused_pose_tick_limits(model):
+    """pa_window_pose_tick refuses windows above 24 frames (PA_EINVAL, nothing launched);
+    StreamingPipeline then runs the four separate launches, and a 30-frame window still
+    solves."""
+    from perseus_amd import _lib, pipeline
+
+    p0, v0, w0 = _init()
+    p = StreamingPipeline(model, graph=True, pose_window=30, init_pose=p0, init_vel=v0, init_angvel=w0, **SIG)
+    assert not p.fused_pose
+    with pytest.raises(_lib.PerseusError, match="L 30"):
+        pipeline.window_pose_tick(p.traj_args, p.y, lam=1e-2, delta=p.gn.out["delta"], info=p.gn.out["info"])
+    truth, _, _ = _truth(3, 3)
+    for k in range(3):
+        _, info = p.tick_keypoints(_keypoints(truth[k]))
+    assert (info == 0).all()
+    p.close()
