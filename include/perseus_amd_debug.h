@@ -29,9 +29,11 @@ int pa_detector_debug_set_trace(pa_detector* d, unsigned long long* trace_dev);
  * per wave, 2 waves per workgroup) receives s_memrealtime stamps at each wave's phases. */
 int pa_debug_trajectory_linearize(const pa_traj_args* args, int mode, unsigned long long* trace_dev, void* stream);
 
-/* Timing only: pa_trajectory_gn_step variant = assembler waves per trajectory (1..4; 0 =
- * the shipped count) + 8 to select the round-2 block-Cholesky solver instead of the
- * shipped block Thomas with swept inverses.  Process-wide. */
+/* Timing / debugging only, process-wide: pa_trajectory_gn_step variant = assembler waves
+ * per trajectory (1..4; 0 = the shipped count) + 8: the round-2 block-Cholesky solver, 16:
+ * the single-chain swept-inverse solver, 32: the two-ended kernel's 4-per-CU form, 64: block
+ * cyclic reduction forced (L <= 24), 128: never cyclic reduction; pa_window_pose_tick: 1024
+ * launches its linearize kernel only, 2048 its GN kernel only. */
 int pa_debug_gn_set_assemblers(int na);
 /* Timing only: pa_trajectory_gn_step writes s_memrealtime stamps (100 MHz), 256 per
  * trajectory, to trace_dev (assembler frame l: slots 2l, 2l+1; solver frame l: 64+4l ..

@@ -820,7 +820,7 @@ __device__ __forceinline__ void traj_unit_wave(const pa_traj_args& a, long u, do
 
 // ---------------------------------------------------------------------------------------
 // Advance: one workgroup per trajectory.  Every element of frames 1 .. L-1 (y, pose, angvel,
-// vel) moves one frame towards l = 0: the 256 threads first load up to ADV_E elements each
+// vel) moves one frame towards l = 0: the workgroup's threads first load up to ADV_E elements each
 // (all loads in flight at once), then, after a barrier, store them one frame down; rounds
 // cover the window in increasing frame order, so no round stores into what a later round
 // reads.  (Round 2's per-element loop waited out one load-store round trip per frame: 18.7

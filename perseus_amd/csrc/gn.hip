@@ -1485,7 +1485,8 @@ int pa_debug_gn_set_assemblers(int na) {
   PA_CHECK((na & 7) <= 4 && na >= 0 && na < 4096 && !((na & 8) && (na & 16)) && !((na & 64) && (na & 128)),
            "gn variant %d: assembler waves (0..4) + 8 * legacy Cholesky or 16 * single-chain solver, 32: "
            "two-ended kernel in its 4-per-CU form, 64: cyclic reduction (L <= 24), 128: never cyclic "
-           "reduction", na);
+           "reduction; pa_window_pose_tick debugging: 1024 its linearize launch only, 2048 its GN launch only",
+           na);
   pa::g_gn_na = na;
   return PA_OK;
 }

@@ -201,7 +201,9 @@ class StreamingPipeline:
             assert self.lin["_keep"][("y", "pose", "vel", "angvel").index(k)].data_ptr() == self.win[k].data_ptr()
         self.gn = pipeline.GNPlan(self.lin, T=n, L=Lw, lam=lam)
         self.gn.out["info"] = self.info_d  # the GN step writes info into the output block
-        self.fused_pose = Lw <= pipeline.TICK_MAX_L and n <= 256
+        # pa_window_pose_tick: one workgroup per camera of up to 24 frames, at most one per CU
+        self.fused_pose = (Lw <= pipeline.TICK_MAX_L
+                           and n <= torch.cuda.get_device_properties(dev).multi_processor_count)
 
     def reset_window(self) -> None:
         """Every frame of every camera's window back to the initial state (keypoints 0, no
