@@ -583,6 +583,9 @@ int launch_stem_pool_rgbd(const RgbdSrc& src, int B, const _Float16* w, const fl
   if (B <= 0) return PA_OK;
   // a few frames (the streaming batch): shorter bands, so the grid still covers the chip
   // (B = 3: 96 workgroups of 2 pooled rows instead of 12 of 16; same arithmetic per row)
+  // (B <= 4: one pooled row per workgroup -- 192 workgroups at B = 3, 5.6 vs 6.7 us for two rows,
+  // bit-identical, profiles/r04stem/)
+  if (B <= 4) return run_stem4<1, 2, true>(nullptr, B, 4, w, bias, out, s, src);
   if (B <= 8) return run_stem4<2, 2, true>(nullptr, B, 4, w, bias, out, s, src);
   if (B <= 24) return run_stem4<4, 2, true>(nullptr, B, 4, w, bias, out, s, src);
   return run_stem4<16, 2, true>(nullptr, B, 4, w, bias, out, s, src);
@@ -618,6 +621,7 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     default: break;
   }
   // small batches: shorter bands (as launch_stem_pool_rgbd)
+  if (B <= 4) return run_stem4<1, 2>(x, B, Cin, w, bias, out, s);
   if (B <= 8) return run_stem4<2, 2>(x, B, Cin, w, bias, out, s);
   if (B <= 24) return run_stem4<4, 2>(x, B, Cin, w, bias, out, s);
   return run_stem4<16, 2>(x, B, Cin, w, bias, out, s);  // also variants 14 / 24 without a trace buffer
