@@ -121,17 +121,31 @@ int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s, bool split_l2) {
     // layer1: the gx kernel on 8 x 16 tiles (4 waves, 9 steps, weights streamed per tap: 96
     // workgroups at B = 3) instead of the weight-resident persistent kernel, whose every
     // workgroup first stages all 73 KB of weights
-    if (!split_l2) return run_gx<8, 16, 1, 64, 2, 2, 64, 3>(a, false, s);
+    if (!split_l2) {
+      // 4 x 16 tiles (192 workgroups at B = 3): 4.7-4.9 vs 5.7-5.9 us for 8 x 16 (profiles/r04sm/)
+      if (g_variant[1] == 36) return run_gx<2, 16, 1, 64, 2, 2, 64, 3>(a, false, s);  // 2 x 16 tiles: 4.8-5.3 us
+      if (g_variant[1] == 35) return run_gx<8, 16, 1, 64, 2, 2, 64, 3>(a, false, s);  // 8 x 16 tiles (A/B)
+      return run_gx<4, 16, 1, 64, 2, 2, 64, 3>(a, false, s);
+    }
     return launch_conv3x3_c64d(a, 0, s);
   }
   if (a.Cin == 128 && a.Cout == 128 && a.Hout == 32 && a.Wout == 32) {
     // layer2: no split -- the batched kernel's 8 x 16 tile form (gx variant 1, 4 waves, 18 steps:
     // 48 workgroups at B = 3), 9.7 us per forward faster than 2 splits + reduce
     // (profiles/r03aa/ab_l2.log) and bit-identical to the batched path
-    if (!split_l2) return launch_conv3x3_gx_l2(a, 1, s);
+    // 2 x 16 tiles (192 workgroups at B = 3): 5.1-5.3 us, 4 x 16 5.8-6.1 (variant 1:36), 8 x 16
+    // 7.4-7.7 (variant 1:35; profiles/r04sm/)
+    if (!split_l2) return launch_conv3x3_gx_l2(a, g_variant[1] == 35 ? 1 : g_variant[1] == 36 ? 5 : 8, s);
     rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 2>(a, s);
   } else if (a.Cin == 256 && a.Cout == 256 && a.Hout == 16 && a.Wout == 16)
-    rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 4>(a, s);
+    // 4 x 16 tiles (192 workgroups at B = 3): 8.9 us with the reduce, 8 x 16 9.9 (variant 3:39),
+    // 16 x 16 11.4 (variant 3:37; profiles/r04sm/)
+    if (g_variant[3] == 37)
+      rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 4>(a, s);
+    else if (g_variant[3] == 39)
+      rc = run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 4>(a, s);
+    else
+      rc = run_gx_part<4, 16, 1, 64, 2, 2, 64, 3, 4>(a, s);
   else if (a.Cin == 512 && a.Cout == 512 && a.Hout == 8 && a.Wout == 8)
     rc = run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8>(a, s);
   else {
@@ -220,14 +234,17 @@ int launch_conv3x3_splitk_x3(const ConvArgs& a, hipStream_t s, const char** knam
   if (a.Cin == 64 && a.Cout == 64 && a.Hout == 64 && a.Wout == 64) {
     // layer1: one 64-channel block, nothing to split; 8 x 16 tiles (4 waves, 18 merged steps)
     if (kname) *kname = "conv3x3x3_l1_small";
-    return run_gx<8, 16, 1, 64, 2, 2, 64, 3, 1, 0, 1, true, true, true>(a, false, s);
+    if (g_variant[1] == 36) return run_gx<8, 16, 1, 64, 2, 2, 64, 3, 1, 0, 1, true, true, true>(a, false, s);  // (A/B)
+    return run_gx<4, 16, 1, 64, 2, 2, 64, 3, 1, 0, 1, true, true, true>(a, false, s);
   }
   if (a.Cin == 128 && a.Cout == 128 && a.Hout == 32 && a.Wout == 32) {
     if (kname) *kname = "conv3x3x3_l2_splitk";
-    rc = run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 2, true, true>(a, s);
+    rc = g_variant[1] == 36 ? run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 2, true, true>(a, s)
+                            : run_gx_part<4, 16, 1, 64, 2, 2, 64, 3, 2, true, true>(a, s);
   } else if (a.Cin == 256 && a.Cout == 256 && a.Hout == 16 && a.Wout == 16) {
     if (kname) *kname = "conv3x3x3_l3_splitk";
-    rc = run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 4, true, true>(a, s);
+    rc = g_variant[1] == 36 ? run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 4, true, true>(a, s)
+                            : run_gx_part<4, 16, 1, 64, 2, 2, 64, 3, 4, true, true>(a, s);
   } else if (a.Cin == 512 && a.Cout == 512 && a.Hout == 8 && a.Wout == 8) {
     if (kname) *kname = "conv3x3x3_l4_splitk";
     rc = run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8, true, true>(a, s);

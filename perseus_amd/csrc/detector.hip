@@ -344,7 +344,9 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
     if constexpr (std::is_same<T, _Float16>::value) {
       const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : a.Hout == 8 ? 4 : 0;
       // g_variant[layer] == 71 (A/B): layer2 split as well, layer1 on the persistent kernel
-      if (layer && small && (g_variant[layer] == 0 || g_variant[layer] == 71) && !(a.epi & EPI_HEAD)) {
+      if (layer && small && (g_variant[layer] == 0 || g_variant[layer] == 71 || (g_variant[layer] >= 35 &&
+                                                                                   g_variant[layer] <= 39)) &&
+          !(a.epi & EPI_HEAD)) {
         const bool split_l2 = g_variant[layer] == 71;
         static const char* names[5] = {"", "conv3x3x_l1_small", "conv3x3x_l2_small", "conv3x3x_l3_splitk",
                                        "conv3x3x_l4_splitk"};
@@ -396,7 +398,8 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       } else if (std::is_same<T, _Float16>::value && small && ho == 16 && g_variant[6] == 0) {
         // layer3's entry in the latency mode: conv_s2x.h's 4 x 16 tiles (twice the workgroups of
         // the batched conv_s2w.h tiles at a few frames: 24 vs 12 at B = 3)
-        PA_RUN(launch_conv3x3s2_x(sa, 0, s, &kn), kn);
+        // 64-channel tiles (48 workgroups at B = 3): 8.0 vs 8.8 us for 128 (variant 3:38, profiles/r04sm/)
+        PA_RUN(launch_conv3x3s2_x(sa, g_variant[3] == 38 ? 0 : 2, s, &kn), kn);
       } else {
         PA_RUN(launch_conv3x3s2_ds<T>(sa, s, &kn), kn);
       }
