@@ -386,8 +386,11 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pos
         if mode.startswith("pose"):
             r["window_frames"] = window
             r["precision"] = pipe.model.precision
-            r["stage"] = ("forward_rgbd_px (latency mode) + pa_window_advance_n + pa_trajectory_linearize + "
-                          "pa_trajectory_gn_step (delta + info) + pa_window_retract_newest")
+            r["stage"] = ("forward_rgbd_px (latency mode) + " +
+                          ("pa_window_pose_tick (advance + linearize, GN step + retract: two launches)"
+                           if getattr(pipe, "fused_pose", False) else
+                           "pa_window_advance_n + pa_trajectory_linearize + pa_trajectory_gn_step (delta + info) + "
+                           "pa_window_retract_newest"))
             r["solved_last_tick"] = int((pipe.info_h.numpy() == 0).sum())
         res[mode] = r
         pipe.close()

@@ -29,6 +29,7 @@ int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const ch
     if (variant & 8) return run_s2x<4, 16, 128, 2, 4, 128, 3, 1, false>(a, xg, s);  // plain (write-back) stores
     if (variant == 7 && a.trace) return run_s2x<4, 16, 128, 2, 4, 128, 3, 1, true, false, 4>(a, xg, s);  // timestamps
     if (variant == 17) return run_s2x<4, 16, 128, 2, 2, 128, 3, 1, true, false, 0, 2>(a, true, s);  // 19.9 vs 18.4 us
+    if (variant == 18) return run_s2x<2, 16, 64, 2, 2, 128, 4>(a, xg, s);  // 2 x 16 x 64 tiles (small batches, A/B)
     switch (variant & 3) {
       case 1: return run_s2x<4, 16, 128, 2, 4, 128, 3, 2>(a, xg, s);
       case 2: return run_s2x<4, 16, 64, 2, 2, 128, 4>(a, xg, s);

@@ -138,16 +138,24 @@ int launch_conv3x3_splitk(const ConvArgs& a, hipStream_t s, bool split_l2) {
     if (!split_l2) return launch_conv3x3_gx_l2(a, g_variant[1] == 35 ? 1 : g_variant[1] == 36 ? 5 : 8, s);
     rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 2>(a, s);
   } else if (a.Cin == 256 && a.Cout == 256 && a.Hout == 16 && a.Wout == 16)
-    // 4 x 16 tiles (192 workgroups at B = 3): 8.9 us with the reduce, 8 x 16 9.9 (variant 3:39),
-    // 16 x 16 11.4 (variant 3:37; profiles/r04sm/)
+    // 2 x 16 tiles (384 workgroups at B = 3): 8.6-8.7 us with the reduce, 4 x 16 8.8-8.9
+    // (variant 3:35), 32-channel 4 x 16 9.4 (3:36), 8 x 16 9.9 (3:39), 16 x 16 11.4 (3:37;
+    // profiles/r04sm/)
     if (g_variant[3] == 37)
       rc = run_gx_part<16, 16, 1, 64, 4, 2, 64, 3, 4>(a, s);
     else if (g_variant[3] == 39)
       rc = run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 4>(a, s);
-    else
+    else if (g_variant[3] == 35)
       rc = run_gx_part<4, 16, 1, 64, 2, 2, 64, 3, 4>(a, s);
+    else
+      rc = run_gx_part<2, 16, 1, 64, 2, 2, 64, 3, 4>(a, s);
   else if (a.Cin == 512 && a.Cout == 512 && a.Hout == 8 && a.Wout == 8)
-    rc = run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8>(a, s);
+    // 4 x 8 tiles of 2 frames (256 workgroups at B = 3): 9.2 us with the reduce vs 9.9 for
+    // 8 x 8 (variant 4:36), 9.2-9.3 for 32-channel 8 x 8 (4:39) and 10.0 for 32-channel 4 x 8
+    // (profiles/r04sm/)
+    rc = g_variant[4] == 36   ? run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8>(a, s)
+         : g_variant[4] == 39 ? run_gx_part<8, 8, 2, 32, 4, 1, 64, 3, 8>(a, s)
+                              : run_gx_part<4, 8, 2, 64, 2, 2, 64, 3, 8>(a, s);
   else {
     set_error("split-K conv: no configuration for %dx%d x %d -> %d", a.Hout, a.Wout, a.Cin, a.Cout);
     return PA_EINVAL;
@@ -239,15 +247,22 @@ int launch_conv3x3_splitk_x3(const ConvArgs& a, hipStream_t s, const char** knam
   }
   if (a.Cin == 128 && a.Cout == 128 && a.Hout == 32 && a.Wout == 32) {
     if (kname) *kname = "conv3x3x3_l2_splitk";
+    // (2 x 16 tiles: 14.2 vs 10.9 us; 32-channel 4 x 16: 11.1, profiles/r04sm/ab_l23s_x3.log)
     rc = g_variant[1] == 36 ? run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 2, true, true>(a, s)
                             : run_gx_part<4, 16, 1, 64, 2, 2, 64, 3, 2, true, true>(a, s);
   } else if (a.Cin == 256 && a.Cout == 256 && a.Hout == 16 && a.Wout == 16) {
     if (kname) *kname = "conv3x3x3_l3_splitk";
+    // (2 x 16 tiles: 14.2 vs 10.9 us; 32-channel 4 x 16: 11.0)
     rc = g_variant[1] == 36 ? run_gx_part<8, 16, 1, 64, 2, 2, 64, 3, 4, true, true>(a, s)
                             : run_gx_part<4, 16, 1, 64, 2, 2, 64, 3, 4, true, true>(a, s);
   } else if (a.Cin == 512 && a.Cout == 512 && a.Hout == 8 && a.Wout == 8) {
     if (kname) *kname = "conv3x3x3_l4_splitk";
-    rc = run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8, true, true>(a, s);
+    // 32-channel 8 x 8 tiles of 2 frames (256 workgroups at B = 3): 11.1-11.2 us with the reduce
+    // vs 12.5-12.7 for 64 channels (variant 4:36) and 11.4-11.5 for 4 x 8 (4:38; profiles/r04sm/)
+    // (32-channel 4 x 8: 11.5)
+    rc = g_variant[4] == 36   ? run_gx_part<8, 8, 2, 64, 4, 2, 64, 3, 8, true, true>(a, s)
+         : g_variant[4] == 38 ? run_gx_part<4, 8, 2, 64, 2, 2, 64, 3, 8, true, true>(a, s)
+                              : run_gx_part<8, 8, 2, 32, 4, 1, 64, 3, 8, true, true>(a, s);
   } else {
     set_error("split-K conv (fp16x3): no configuration for %dx%d x %d -> %d", a.Hout, a.Wout, a.Cin, a.Cout);
     return PA_EINVAL;
@@ -264,17 +279,23 @@ int launch_conv3x3s2_small_x3(const ConvS2Args& a, hipStream_t s, const char** k
   if (a.Hout == 32 && a.Cin == 64 && a.Cout == 128) {
     // one input-channel block: unsplit, 64-channel tiles on 4 waves (B = 3: 96 workgroups of 30 steps)
     if (kname) *kname = "conv3x3s2x3_l2_small";
-    return run_s2x<4, 16, 64, 2, 2, 64, 3, 1, true, true>(a, false, s);
+    // 2 x 16 tiles (192 workgroups at B = 3): 8.2 vs 10.5 us for 4 x 16 (variant 2:37, profiles/r04sm/)
+    if (g_variant[2] == 37) return run_s2x<4, 16, 64, 2, 2, 64, 3, 1, true, true>(a, false, s);
+    return run_s2x<2, 16, 64, 2, 2, 64, 3, 1, true, true>(a, false, s);
   }
   int rc, ns;
   if (a.Hout == 16 && a.Cin == 128 && a.Cout == 256) {
     if (kname) *kname = "conv3x3s2x3_l3_splitk";
     ns = 2;
-    rc = run_s2x_part<4, 16, 64, 2, 2, 64, 3, 2, true>(a, s);
+    // 2 x 16 tiles: 11.9 vs 14.2 us with the reduce for 4 x 16 (variant 3:37)
+    rc = g_variant[3] == 37 ? run_s2x_part<4, 16, 64, 2, 2, 64, 3, 2, true>(a, s)
+                            : run_s2x_part<2, 16, 64, 2, 2, 64, 3, 2, true>(a, s);
   } else if (a.Hout == 8 && a.Cin == 256 && a.Cout == 512) {
     if (kname) *kname = "conv3x3s2x3_l4_splitk";
     ns = 4;
-    rc = run_s2x_part<8, 8, 64, 2, 2, 64, 3, 4, true>(a, s);
+    // 4 x 8 tiles: 11.7 vs 14.1 us with the reduce for 8 x 8 (variant 4:37)
+    rc = g_variant[4] == 37 ? run_s2x_part<8, 8, 64, 2, 2, 64, 3, 4, true>(a, s)
+                            : run_s2x_part<4, 8, 64, 2, 2, 64, 3, 4, true>(a, s);
   } else {
     set_error("s2x3 small batch: no configuration for %dx%d x %d -> %d", a.Hout, a.Wout, a.Cin, a.Cout);
     return PA_EINVAL;
@@ -292,11 +313,15 @@ int launch_conv3x3s2_small(const ConvS2Args& a, hipStream_t s, const char** knam
     // workgroups of 10 steps, 6.5 us; the batched kernel runs 12 workgroups of 4 tiles, 40
     // steps, 17.8 us)
     if (kname) *kname = "conv3x3s2x_l2_small";
-    return run_s2x<4, 16, 64, 2, 2, 64, 3>(a, false, s);
+    // 2 x 16 tiles (192 workgroups at B = 3): 4.7 vs 5.8 us for 4 x 16 (variant 2:37, profiles/r04sm/)
+    if (g_variant[2] == 37) return run_s2x<4, 16, 64, 2, 2, 64, 3>(a, false, s);
+    return run_s2x<2, 16, 64, 2, 2, 64, 3>(a, false, s);
   }
   if (a.Hout == 8 && a.Cin == 256 && a.Cout == 512) {
     if (kname) *kname = "conv3x3s2x_l4_splitk";
-    const int rc = run_s2x_part<8, 8, 64, 2, 2, 64, 3, 4>(a, s);
+    // 4 x 8 tiles: 8.6 vs 10.0 us with the reduce for 8 x 8 (variant 4:37)
+    const int rc = g_variant[4] == 37 ? run_s2x_part<8, 8, 64, 2, 2, 64, 3, 4>(a, s)
+                                      : run_s2x_part<4, 8, 64, 2, 2, 64, 3, 4>(a, s);
     if (rc != PA_OK) return rc;
     return launch_reduce(a.part, 4, (size_t)a.B * 64 * 512, a.bias, nullptr, (_Float16*)a.out, 512, a.bias2,
                          (_Float16*)a.out2, s);

@@ -396,10 +396,10 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
         sa.part = d->part;
         PA_RUN(launch_conv3x3s2_small(sa, s, &kn), kn);
       } else if (std::is_same<T, _Float16>::value && small && ho == 16 && g_variant[6] == 0) {
-        // layer3's entry in the latency mode: conv_s2x.h's 4 x 16 tiles (twice the workgroups of
-        // the batched conv_s2w.h tiles at a few frames: 24 vs 12 at B = 3)
-        // 64-channel tiles (48 workgroups at B = 3): 8.0 vs 8.8 us for 128 (variant 3:38, profiles/r04sm/)
-        PA_RUN(launch_conv3x3s2_x(sa, g_variant[3] == 38 ? 0 : 2, s, &kn), kn);
+        // layer3's entry in the latency mode: conv_s2x.h tiles, 2 x 16 x 64 (96 workgroups at
+        // B = 3, vs 12 for the batched conv_s2w.h tiles): 6.2 us vs 7.9 for 4 x 16 x 64 (variant
+        // 3:71) and 8.8 for 4 x 16 x 128 (3:38), profiles/r04sm/
+        PA_RUN(launch_conv3x3s2_x(sa, g_variant[3] == 38 ? 0 : g_variant[3] == 71 ? 2 : 18, s, &kn), kn);
       } else {
         PA_RUN(launch_conv3x3s2_ds<T>(sa, s, &kn), kn);
       }
