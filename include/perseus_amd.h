@@ -265,6 +265,23 @@ int pa_window_retract_newest(int T, int L, const double* delta_dev, const int32_
 int pa_window_pose_tick(const pa_traj_args* args, const float* y_new_dev, double lambda, double* delta_dev,
                         int32_t* info_dev, double* newest_pose_dev, void* stream);
 
+/* The same tick split around the keypoints, so that most of it runs before they exist (the
+ * streaming graph runs the pre half on a second stream beside the detector forward):
+ *   pa_window_pose_tick_pre: the window advances WITHOUT the new keypoints, every factor but
+ *     frame L-1's projections is linearized (those are marked status 3 for now), and the GN
+ *     system is assembled and reduced by block cyclic reduction down to frame L-1 (the root),
+ *     into ws (pa_window_pose_tick_workspace bytes);
+ *   pa_window_pose_tick_post: y_new lands as frame L-1's keypoints, its projection factors
+ *     are linearized into the factor outputs (as pa_trajectory_linearize writes them), added
+ *     to the reduced root, and the step is solved (delta, info) and retracted (newest_pose).
+ * Pre then post on the same window = pa_window_pose_tick up to f64 rounding (another
+ * elimination order; the window's keypoints and factor outputs are bit-identical; info names
+ * a frame whose pivot failed in that order).  Same limits as pa_window_pose_tick. */
+size_t pa_window_pose_tick_workspace(int T, int L);
+int pa_window_pose_tick_pre(const pa_traj_args* args, double lambda, void* ws_dev, size_t ws_bytes, void* stream);
+int pa_window_pose_tick_post(const pa_traj_args* args, const float* y_new_dev, const void* ws_dev, size_t ws_bytes,
+                             double* delta_dev, int32_t* info_dev, double* newest_pose_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

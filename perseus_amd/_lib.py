@@ -76,6 +76,10 @@ _SIGS = {
     "pa_host_device_pointer": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "pa_window_pose_tick": (C.c_int, [C.POINTER(TrajArgs), C.c_void_p, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p]),
+    "pa_window_pose_tick_workspace": (C.c_size_t, [C.c_int, C.c_int]),
+    "pa_window_pose_tick_pre": (C.c_int, [C.POINTER(TrajArgs), C.c_double, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "pa_window_pose_tick_post": (C.c_int, [C.POINTER(TrajArgs), C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]),
     "pa_loss_statistics_workspace": (C.c_size_t, [C.c_longlong]),
     "pa_loss_statistics": (C.c_int, [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "pa_proj_linearize": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,

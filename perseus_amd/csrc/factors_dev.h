@@ -889,7 +889,7 @@ __device__ __forceinline__ void window_advance_body(int t, int e, int nthr, int 
     }
     __syncthreads();
   }
-  if (e < ny) yt[(L - 1) * ny + e] = y_new[(size_t)t * ny + e];
+  if (y_new && e < ny) yt[(L - 1) * ny + e] = y_new[(size_t)t * ny + e];  // (null: the split tick's post half lands it)
   __syncthreads();
   if (e == 0 && L >= 2) {
     const Pose T1 = load_pose(pt + (L - 2) * 12);
@@ -923,19 +923,18 @@ __device__ __forceinline__ void window_advance_body(int t, int e, int nthr, int 
 // keep their values.
 // newest (optional): each trajectory's last-frame pose after the update (T, 12), the
 // streaming tick's output, so it needs no gather of the strided window
-__device__ __forceinline__ void window_retract_one(long f, int L, const double* __restrict__ delta,
-                                                   const int32_t* __restrict__ info, double* pose, double* angvel,
-                                                   double* vel, double* newest) {
+// (d: frame f's 12 delta values, anywhere; solved: its trajectory's info == 0)
+__device__ __forceinline__ void window_retract_frame(long f, int L, const double* d, bool solved, double* pose,
+                                                     double* angvel, double* vel, double* newest) {
   const long t = f / L;
   double* o = pose + f * 12;
   double* no = (newest && f - t * L == L - 1) ? newest + t * 12 : nullptr;
-  if (info && info[t] != 0) {  // unsolved: the window stays
+  if (!solved) {  // unsolved: the window stays
     if (no)
 #pragma unroll
       for (int i = 0; i < 12; ++i) no[i] = o[i];
     return;
   }
-  const double* d = delta + f * 12;
   const V3 dw = load3(d), dv = load3(d + 3);
   const Pose P = compose(load_pose(o), pose_exp(dw, dv, ang(dw)));
   double v[12];
@@ -954,6 +953,12 @@ __device__ __forceinline__ void window_retract_one(long f, int L, const double* 
     angvel[f * 3 + i] += d[6 + i];
     vel[f * 3 + i] += d[9 + i];
   }
+}
+
+__device__ __forceinline__ void window_retract_one(long f, int L, const double* __restrict__ delta,
+                                                   const int32_t* __restrict__ info, double* pose, double* angvel,
+                                                   double* vel, double* newest) {
+  window_retract_frame(f, L, delta + f * 12, !(info && info[f / L] != 0), pose, angvel, vel, newest);
 }
 
 }  // namespace pa

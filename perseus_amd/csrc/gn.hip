@@ -1112,14 +1112,14 @@ __device__ __forceinline__ void gn_mm_store(double* out, const gn_d4& c, double 
 }
 
 // LDS of gn_cr_run: fb (S | C | b per frame) and the pool (assembly staging, then the level data)
-template <int RP, int NS>
+template <int RP, int NS, bool ROOT = false>
 struct GnCrLds {
   static constexpr int BLK = 2 * gn::NB + gn::NV;
   static constexpr int LM = GN_CR_LMAX, W = GN_CR_W;
   static constexpr int CHD = (int)(sizeof(GnChainLds) / sizeof(double));
   static constexpr int STGD = (int)(sizeof(GnStage<RP>) / sizeof(double));
   static constexpr int FR = 2 * gn::NB + gn::NV;
-  static constexpr bool PAIR = NS == W && 2 * W >= LM;
+  static constexpr bool PAIR = !ROOT && NS == W && 2 * W >= LM;
   static constexpr int SLAB0 = 2 * FR + CHD > STGD ? 2 * FR + CHD : STGD;
   static constexpr int SLAB = (SLAB0 + 1) / 2 * 2;
   static constexpr int POST = LM * FR + W * CHD;
@@ -1127,8 +1127,38 @@ struct GnCrLds {
   static constexpr int POOL = PAIR ? W * SLAB : (POST > STG ? POST : STG);
 };
 
-// trajectory t on this workgroup (64 * GN_CR_W threads); fb / pool: GnCrLds<RP, NS> in LDS
-template <int RP, int NS>
+// The split streaming tick (pa_window_pose_tick_pre / _post): per trajectory, the reduced
+// system the pre half leaves for the post half in the workspace a.ws (doubles): PM | QM | z
+// of every eliminated frame (the pool, L x FR), the root's S | b, the failure word
+constexpr int GN_TICK_WSD = GN_CR_LMAX * (2 * gn::NB + gn::NV) + gn::NB + gn::NV + 2;
+
+// the level lists: frames active at each level, the parity of the eliminated positions
+// (pe), the level count.  Shipped order: n even -> the odd positions, n odd -> the even ones
+// (PAIR: level 0 the odd ones whatever the parity).  ROOT (the split tick): n even -> the
+// even positions, n odd -> the odd ones, so position n - 1, frame L - 1, is never eliminated
+// and stays as the root of the reduction (24 -> 12 -> 6 -> 3 -> 2 -> 1: one level more).
+template <bool PAIR, bool ROOT>
+__device__ __forceinline__ int gn_cr_lists(int L, signed char (*lst)[GN_CR_LMAX], int* lcnt, int* lpe) {
+  int n = L, lv = 0;
+  for (int l = 0; l < L; ++l) lst[0][l] = (signed char)l;
+  while (n > 1) {
+    const int pe = ROOT ? (n & 1) : ((PAIR && lv == 0) || !(n & 1) ? 1 : 0);
+    int m = 0;
+    for (int p = 0; p < n; ++p)
+      if ((p & 1) != pe) lst[lv + 1][m++] = lst[lv][p];
+    lcnt[lv] = n;
+    lpe[lv] = pe;
+    n = m;
+    ++lv;
+  }
+  lcnt[lv] = 1;
+  return lv;
+}
+
+// trajectory t on this workgroup (64 * GN_CR_W threads); fb / pool: GnCrLds<RP, NS, ROOT> in LDS.
+// ROOT (pa_window_pose_tick_pre): the ROOT level order, and after the last level the reduced
+// system goes to the workspace (GN_TICK_WSD per trajectory) instead of being solved.
+template <int RP, int NS, bool ROOT = false>
 __device__ __forceinline__ void gn_cr_run(const GnArgs& a, int t, double (*fb)[2 * gn::NB + gn::NV], double* pool) {
   using namespace gn;
   constexpr int BLK = 2 * NB + NV;
@@ -1141,7 +1171,7 @@ __device__ __forceinline__ void gn_cr_run(const GnArgs& a, int t, double (*fb)[2
   // level 0 needs no barrier of its own.  Its slab of the pool is its staging, then the
   // PM | QM | z of frames 2w + 1 and 2w and its sweep scratch.  Otherwise (the general-K
   // instance: its staging does not fit 12 times) NS waves assemble, then every wave starts.
-  constexpr bool PAIR = NS == W && 2 * W >= LM;
+  constexpr bool PAIR = !ROOT && NS == W && 2 * W >= LM;
   constexpr int SLAB0 = 2 * FR + CHD > STGD ? 2 * FR + CHD : STGD;
   constexpr int SLAB = (SLAB0 + 1) / 2 * 2;
   constexpr int POST = LM * FR + W * CHD;
@@ -1149,7 +1179,7 @@ __device__ __forceinline__ void gn_cr_run(const GnArgs& a, int t, double (*fb)[2
   constexpr int POOL = PAIR ? W * SLAB : (POST > STG ? POST : STG);
   constexpr int NOFAIL = 0x7fffffff;
   static_assert(NS <= W, "assembler waves");
-  static_assert(POOL == GnCrLds<RP, NS>::POOL && BLK == GnCrLds<RP, NS>::BLK, "LDS layout");
+  static_assert(POOL == GnCrLds<RP, NS, ROOT>::POOL && BLK == GnCrLds<RP, NS, ROOT>::BLK, "LDS layout");
   __shared__ signed char lst[8][LM];  // active frames per level
   __shared__ int lcnt[8], lpe[8];
   __shared__ int nlev_s, fail;
@@ -1163,20 +1193,7 @@ __device__ __forceinline__ void gn_cr_run(const GnArgs& a, int t, double (*fb)[2
   GnChainLds& C = *reinterpret_cast<GnChainLds*>(PAIR ? pool + wv * SLAB + 2 * FR : pool + LM * FR + wv * CHD);
   auto dl = [&](int f) __attribute__((always_inline)) -> double* { return fb[f]; };
   if (threadIdx.x == 0) {
-    int n = L, lv = 0;
-    for (int l = 0; l < L; ++l) lst[0][l] = (signed char)l;
-    while (n > 1) {
-      const int pe = (PAIR && lv == 0) || !(n & 1) ? 1 : 0;  // parity of the eliminated positions
-      int m = 0;
-      for (int p = 0; p < n; ++p)
-        if ((p & 1) != pe) lst[lv + 1][m++] = lst[lv][p];
-      lcnt[lv] = n;
-      lpe[lv] = pe;
-      n = m;
-      ++lv;
-    }
-    lcnt[lv] = 1;
-    nlev_s = lv;
+    nlev_s = gn_cr_lists<PAIR, ROOT>(L, lst, lcnt, lpe);
     fail = NOFAIL;
   }
   // the level lists and `fail` are in place before any wave eliminates or reads them (LDS
@@ -1297,6 +1314,14 @@ __device__ __forceinline__ void gn_cr_run(const GnArgs& a, int t, double (*fb)[2
     __syncthreads();
     if (wv == 0) gn_stamp(a, t, 11 + 2 * lv);
   }
+  if constexpr (ROOT) {  // the reduced system to the workspace (the root is frame L - 1)
+    double* w = a.ws + (size_t)t * GN_TICK_WSD;
+    for (int e = threadIdx.x; e < L * FR / 2; e += 64 * W)
+      reinterpret_cast<gn_d2*>(w)[e] = reinterpret_cast<const gn_d2*>(pool)[e];
+    for (int e = threadIdx.x; e < NB + NV; e += 64 * W) w[LM * FR + e] = e < NB ? fb[L - 1][e] : fb[L - 1][NB + e];
+    if (threadIdx.x == 0) reinterpret_cast<int*>(w + LM * FR + NB + NV)[0] = fail == NOFAIL ? 0 : fail;
+    return;
+  }
   if (fail == NOFAIL && wv == 0) {  // the last active frame: delta = S^-1 b (over its S block)
     const int ff = lst[nlev][0];
     double sv[4];
@@ -1369,6 +1394,10 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void gn_cr_kernel(GnArgs a) {
 // the factors, delta, info and the newest poses are bit for bit the four-launch sequence's
 // (tests/test_streaming_pose_gpu.py).
 constexpr int TICK_LIN_W = 6;
+// y_new null (the split tick's pre half): the window advances without the new keypoints, and
+// frame L - 1's projection factors (evaluated on the stale keypoints the slot still holds)
+// are marked status 3 afterwards, so the GN assembly gives them zero rows; the post half
+// evaluates them on y_new.
 __global__ __launch_bounds__(64 * TICK_LIN_W) void pose_tick_lin_kernel(pa_traj_args ta, const float* __restrict__ y_new) {
   static_assert((trj::STAGE + 4 * trj::UNIT) * 8 <= 96 * 1024, "factor staging");
   __shared__ __attribute__((aligned(16))) double st[trj::STAGE + 4 * trj::UNIT];
@@ -1410,6 +1439,10 @@ __global__ __launch_bounds__(64 * TICK_LIN_W) void pose_tick_lin_kernel(pa_traj_
     if (wv - 2 <= wp) traj_unit_wave(a1, wv - 2, st + trj::STAGE + (wv - 2) * trj::UNIT, nullptr);
     lds_barrier();
   }
+  if (!y_new) {  // (uniform)
+    __syncthreads();  // the unit waves' status stores come first
+    if ((int)threadIdx.x < K) a1.status[(long)(L - 1) * K + threadIdx.x] = 3;
+  }
 }
 
 template <int RP>
@@ -1424,6 +1457,156 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void pose_tick_gn_kernel(GnArgs g,
   __syncthreads();
   if ((int)threadIdx.x < L)
     window_retract_one((long)t * L + threadIdx.x, L, g.delta, g.info, pose, angvel, vel, newest);
+}
+
+// The split tick.  pa_window_pose_tick_pre (before the keypoints exist: it runs beside the
+// detector forward on a second stream of the tick's graph) = pose_tick_lin_kernel(null) +
+// pose_tick_pre_kernel: every factor but the newest frame's projections, assembled and
+// reduced by cyclic reduction in the ROOT order down to frame L - 1 alone.  A projection
+// factor touches only its own frame's diagonal block, and the root's S and b enter the
+// reduction only additively (no elimination reads them), so the newest frame's projection
+// rows can be added to the reduced root at the end:
+//   pose_tick_post_kernel  y_new lands in the window, its K projection factors (the factor
+//        outputs, as the linearize writes them), S_root += Jp^T Jp and b_root -= Jp^T rp on the
+//        pose block, delta_root = S_root^-1 b_root, back substitution, delta / info, retract.
+// The same normal equations as pa_window_pose_tick, another elimination order and f64
+// rounding (tests/test_streaming_pose_gpu.py: within 1e-9 of its delta).
+template <int RP>
+__global__ __launch_bounds__(64 * GN_CR_W, 1) void pose_tick_pre_kernel(GnArgs g) {
+  constexpr int NS = RP <= 34 ? 12 : 8;
+  using Ld = GnCrLds<RP, NS, true>;
+  __shared__ __attribute__((aligned(16))) double fb[Ld::LM][Ld::BLK];
+  __shared__ __attribute__((aligned(16))) double pool[Ld::POOL];
+  gn_cr_run<RP, NS, true>(g, blockIdx.x, fb, pool);
+}
+
+__global__ __launch_bounds__(64 * GN_CR_W, 1) void pose_tick_post_kernel(pa_traj_args ta, const float* __restrict__ y_new,
+                                                                          const double* __restrict__ ws, double* delta,
+                                                                          int32_t* info, double* newest) {
+  using namespace gn;
+  constexpr int LM = GN_CR_LMAX, W = GN_CR_W, FR = 2 * NB + NV, KP = 2 * GN_KMAX;
+  __shared__ __attribute__((aligned(16))) double pool[LM * FR];  // PM | QM | z per eliminated frame
+  __shared__ __attribute__((aligned(16))) double dl[LM][NV];     // delta per frame
+  __shared__ __attribute__((aligned(16))) double sr[NB + NV];    // the root's S | b
+  __shared__ __attribute__((aligned(16))) double jt[7][KP];      // newest frame: Jp^T (6 x 2K) | rp
+  __shared__ __attribute__((aligned(16))) GnChainLds C;
+  __shared__ signed char lst[8][LM];
+  __shared__ int lcnt[8], lpe[8];
+  __shared__ int nlev_s, fail_s;
+  const int t = blockIdx.x, L = ta.L, K = ta.n_kp, ny = 2 * K;
+  const int wv = threadIdx.x >> 6, i = threadIdx.x & 63;
+  const long f0 = (long)t * L, fn = f0 + L - 1;
+  const double* w = ws + (size_t)t * GN_TICK_WSD;
+  // the pre half's reduced system -> LDS (every load in flight before the projections)
+  for (int e = threadIdx.x; e < L * FR / 2; e += 64 * W)
+    reinterpret_cast<gn_d2*>(pool)[e] = reinterpret_cast<const gn_d2*>(w)[e];
+  for (int e = threadIdx.x; e < NB + NV; e += 64 * W) sr[e] = w[LM * FR + e];
+  if (threadIdx.x == 0) {
+    nlev_s = gn_cr_lists<false, true>(L, lst, lcnt, lpe);
+    fail_s = reinterpret_cast<const int*>(w + LM * FR + NB + NV)[0];
+  }
+  double s = 0.0;  // wave 0, lane o < 42: entry o of [Jp^T Jp | Jp^T rp] (6 x 7, row-major)
+  if (wv == 0) {
+    // y_new lands (pa_window_advance's last step) and frame L - 1's projection factors:
+    // lane k, traj_unit_wave's evaluation
+    if (i < ny) const_cast<float*>(ta.y)[fn * ny + i] = y_new[(size_t)t * ny + i];
+    if (i < K) {
+      const Cam cam = load_cam(ta.K, ta.tcam, ta.isig_proj);
+      const Pose T = load_pose(ta.pose + fn * 12);
+      const V3 pb = load3(ta.corners + 3 * i);
+      const float px = kornia_denorm(y_new[(size_t)t * ny + 2 * i], ta.W);
+      const float py = kornia_denorm(y_new[(size_t)t * ny + 2 * i + 1], ta.H);
+      const bool off = ta.nvalid ? L - 1 < L - ta.nvalid[t] : false;
+      double r[2], J[12], e;
+      int32_t st;
+      proj_eval(T, pb, (double)px, (double)py, cam, r, J, e, st);
+      if (off) {
+        r[0] = r[1] = 0.0;
+#pragma unroll
+        for (int c = 0; c < 12; ++c) J[c] = 0.0;
+        e = 0.0;
+        st = 2;
+      }
+      const long u = fn * K + i;
+      ta.r_proj[u * 2] = r[0];
+      ta.r_proj[u * 2 + 1] = r[1];
+#pragma unroll
+      for (int c = 0; c < 12; ++c) ta.j_proj[u * 12 + c] = J[c];
+      if (ta.err_proj) ta.err_proj[u] = e;
+      ta.status[u] = st;
+      // the GN assembly's rows: a failed projection (status != 0) gives zero rows
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        jt[c][2 * i] = st == 0 ? J[c * 2] : 0.0;
+        jt[c][2 * i + 1] = st == 0 ? J[c * 2 + 1] : 0.0;
+      }
+      jt[6][2 * i] = st == 0 ? r[0] : 0.0;
+      jt[6][2 * i + 1] = st == 0 ? r[1] : 0.0;
+    }
+    wave_order();
+    if (i < 42) {
+      const int ra = i < 36 ? i / 6 : i - 36, cb = i < 36 ? i - 6 * (i / 6) : 6;
+      for (int q = 0; q < ny; ++q) s += jt[ra][q] * jt[cb][q];
+    }
+  }
+  __syncthreads();  // the reduced system, the level lists
+  const int nlev = nlev_s;
+  const bool act = i < 36;
+  const int ii = act ? i : 35;
+  const int r = ii / 3, c0 = 4 * (ii - 3 * (ii / 3));
+  if (wv == 0) {
+    // the newest frame's projections into the root (S += Jp^T Jp on the pose block, b -= Jp^T rp)
+    if (i < 36) sr[(i / 6) * NV + i - 6 * (i / 6)] += s;
+    else if (i < 42) sr[NB + i - 36] -= s;
+    wave_order();
+    if (fail_s == 0) {  // delta_root = S^-1 b
+      double sv[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sv[c] = sr[r * NV + c0 + c];
+      const double b = sr[NB + r];
+      if (!gn_sweep(sv, C.rk2, r, c0, act)) {
+        if (i == 0) fail_s = L;
+      } else {
+        const double z = gn_finish(sv, b, C, r, c0, act);
+        wave_order();
+        if (act && c0 == 0) dl[L - 1][r] = z;
+      }
+    }
+  }
+  __syncthreads();
+  const int inf = fail_s;
+  if (!inf) {
+    for (int lv = nlev - 1; lv >= 0; --lv) {  // gn_cr_run's back substitution
+      const int n = lcnt[lv], pe = lpe[lv];
+      const int ne = pe ? n / 2 : (n + 1) / 2;
+      for (int e = wv; e < ne; e += W) {
+        const int pos = 2 * e + pe;
+        const int fi = lst[lv][pos];
+        const int fp = pos > 0 ? lst[lv][pos - 1] : -1, fq = pos + 1 < n ? lst[lv][pos + 1] : -1;
+        const double* o = pool + fi * FR;
+        if (i < NV) {
+          double d0 = o[2 * NB + i], d1 = 0.0;
+          if (fp >= 0)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) d0 -= o[k * NV + i] * dl[fp][k];
+          if (fq >= 0)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) d1 += o[NB + k * NV + i] * dl[fq][k];
+          dl[fi][i] = d0 - d1;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  double* dt = delta + (size_t)f0 * NV;
+  for (int e = threadIdx.x; e < L * NV; e += 64 * W) {
+    const int l = e / NV;
+    dt[e] = inf ? NAN : dl[l][e - l * NV];
+  }
+  if (threadIdx.x == 0) info[t] = inf;
+  if ((int)threadIdx.x < L)  // (delta from LDS: the back substitution's last barrier is behind it)
+    window_retract_frame(f0 + threadIdx.x, L, dl[threadIdx.x], inf == 0, const_cast<double*>(ta.pose),
+                         const_cast<double*>(ta.angvel), const_cast<double*>(ta.vel), newest);
 }
 
 // assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * legacy;
@@ -1520,6 +1703,61 @@ int pa_window_pose_tick(const pa_traj_args* ta, const float* y_new, double lambd
   else
     hipLaunchKernelGGL(pa::pose_tick_gn_kernel<2 * pa::GN_KMAX + 18>, dim3(T), dim3(64 * pa::GN_CR_W), 0, s, g, pose,
                        angvel, vel, newest_pose);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+size_t pa_window_pose_tick_workspace(int T, int L) {
+  return (T > 0 && L > 0) ? (size_t)T * pa::GN_TICK_WSD * sizeof(double) : 0;
+}
+
+// the checks of pa_window_pose_tick
+static int pose_tick_check(const pa_traj_args* ta, const char* who) {
+  PA_CHECK(ta, "%s: null args", who);
+  const int T = ta->T, L = ta->L, K = ta->n_kp;
+  PA_CHECK(T >= 0 && T <= pa::g_gn_cus() && L >= 2 && L <= pa::GN_CR_LMAX && K >= 0 && K <= pa::GN_KMAX,
+           "%s: T %d (<= %d CUs), L %d (2..%d), n_kp %d (<= %d)", who, T, pa::g_gn_cus(), L, pa::GN_CR_LMAX, K,
+           pa::GN_KMAX);
+  PA_CHECK(ta->y && ta->pose && ta->vel && ta->angvel && ta->corners && ta->K && ta->nvalid,
+           "%s: null window / model pointer", who);
+  PA_CHECK((K == 0 || (ta->r_proj && ta->j_proj && ta->status)) && ta->r_dyn && ta->j_dyn0 && ta->j_dyn1 &&
+               ta->j_dyn2 && ta->j_dyn3 && ta->r_cv && ta->j_cv0 && ta->j_cv1,
+           "%s: the factor outputs and every Jacobian are required", who);
+  return PA_OK;
+}
+
+int pa_window_pose_tick_pre(const pa_traj_args* ta, double lambda, void* ws, size_t ws_bytes, void* stream) {
+  const int rc = pose_tick_check(ta, "pose tick pre");
+  if (rc != PA_OK) return rc;
+  const int T = ta->T, L = ta->L, K = ta->n_kp;
+  if (T == 0) return PA_OK;
+  PA_CHECK(lambda >= 0.0, "pose tick pre: lambda %g < 0", lambda);
+  PA_CHECK(ws && ws_bytes >= pa_window_pose_tick_workspace(T, L), "pose tick pre: workspace %zu < %zu", ws_bytes,
+           pa_window_pose_tick_workspace(T, L));
+  const pa::GnArgs g{T,     L,     K,     ta->r_proj, ta->j_proj, ta->status, ta->r_dyn, ta->j_dyn0,
+                     ta->j_dyn1, ta->j_dyn2, ta->j_dyn3, ta->r_cv, ta->j_cv0, ta->j_cv1, lambda, nullptr,
+                     nullptr, nullptr, nullptr, nullptr, (double*)ws, nullptr};
+  const hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(pa::pose_tick_lin_kernel, dim3(T), dim3(64 * pa::TICK_LIN_W), 0, s, *ta, nullptr);
+  if (K == 8)
+    hipLaunchKernelGGL(pa::pose_tick_pre_kernel<34>, dim3(T), dim3(64 * pa::GN_CR_W), 0, s, g);
+  else
+    hipLaunchKernelGGL(pa::pose_tick_pre_kernel<2 * pa::GN_KMAX + 18>, dim3(T), dim3(64 * pa::GN_CR_W), 0, s, g);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+int pa_window_pose_tick_post(const pa_traj_args* ta, const float* y_new, const void* ws, size_t ws_bytes,
+                             double* delta, int32_t* info, double* newest_pose, void* stream) {
+  const int rc = pose_tick_check(ta, "pose tick post");
+  if (rc != PA_OK) return rc;
+  const int T = ta->T, L = ta->L;
+  if (T == 0) return PA_OK;
+  PA_CHECK(y_new && delta && info, "pose tick post: null y_new / delta / info");
+  PA_CHECK(ws && ws_bytes >= pa_window_pose_tick_workspace(T, L), "pose tick post: workspace %zu < %zu", ws_bytes,
+           pa_window_pose_tick_workspace(T, L));
+  hipLaunchKernelGGL(pa::pose_tick_post_kernel, dim3(T), dim3(64 * pa::GN_CR_W), 0, (hipStream_t)stream, *ta, y_new,
+                     (const double*)ws, delta, info, newest_pose);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -225,6 +225,33 @@ def window_pose_tick(args, y_new: torch.Tensor, *, lam: float, delta: torch.Tens
                    "pa_window_pose_tick")
 
 
+def window_pose_tick_workspace(T: int, L: int, device) -> torch.Tensor:
+    """The reduced system pa_window_pose_tick_pre leaves for _post (bytes as a u8 tensor)."""
+    n = int(_lib.lib().pa_window_pose_tick_workspace(int(T), int(L)))
+    return torch.empty(max(n, 1), dtype=torch.uint8, device=device)
+
+
+def window_pose_tick_pre(args, ws: torch.Tensor, *, lam: float) -> None:
+    """pa_window_pose_tick_pre on the device's current stream: the window advances without the
+    new keypoints, every factor but the newest frame's projections, the GN system reduced to
+    the newest frame (into ws)."""
+    dev = ws.device
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pa_window_pose_tick_pre(C.byref(args), float(lam), ws.data_ptr(), ws.numel(),
+                                                      _lib.stream_of(dev)), "pa_window_pose_tick_pre")
+
+
+def window_pose_tick_post(args, y_new: torch.Tensor, ws: torch.Tensor, *, delta: torch.Tensor, info: torch.Tensor,
+                          newest: torch.Tensor | None = None) -> None:
+    """pa_window_pose_tick_post on the device's current stream: y_new lands, the newest frame's
+    projection factors join the reduced system, solve (delta, info), retract (newest)."""
+    dev = y_new.device
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pa_window_pose_tick_post(C.byref(args), y_new.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                       delta.data_ptr(), info.data_ptr(), _lib.ptr(newest),
+                                                       _lib.stream_of(dev)), "pa_window_pose_tick_post")
+
+
 def window_retract(win: dict, delta: torch.Tensor, info: torch.Tensor | None = None,
                    newest: torch.Tensor | None = None) -> None:
     """pa_window_retract on the device's current stream: pose <- pose Exp(delta[:6]),

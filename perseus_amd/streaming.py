@@ -53,7 +53,7 @@ class StreamingPipeline:
                  pose_window: int = 0, K=None, corners=None, dt: float = 1.0 / 30.0, vel_frame: str = "world",
                  proj_sigma: float = 1.0, dyn_sigma: float = 0.1, cv_sigma: float = 0.1, lam: float = 1e-2,
                  init_pose=None, init_vel=None, init_angvel=None, split_k: bool = True,
-                 zero_copy: bool | None = None):
+                 zero_copy: bool | None = None, split_pose: bool = True):
         if not torch.cuda.is_available():
             raise RuntimeError("StreamingPipeline needs a ROCm GPU (no CPU fallback)")
         cam_K = K  # (the name K is the keypoint count below)
@@ -126,6 +126,8 @@ class StreamingPipeline:
         if model.num_channels != 4:
             raise ValueError("StreamingPipeline feeds RGBD (num_channels=4)")
         self.pose_L = int(pose_window)
+        self._split_pose_req = bool(split_pose)
+        self.fused_pose = self.split_pose = False
         if self.pose_L:
             self._init_pose_stage(cam_K, corners, dt, vel_frame, proj_sigma, dyn_sigma, cv_sigma, lam, init_pose,
                                   init_vel, init_angvel)
@@ -142,24 +144,51 @@ class StreamingPipeline:
             self.graph = g
 
     def _enqueue(self):
-        """H2D, preprocess + forward + denormalize, [pose stage], D2H on the current stream."""
+        """H2D, preprocess + forward + denormalize, [pose stage], D2H on the current stream.
+        Split pose tick: the forward runs on a second stream while this one runs the pre half
+        (everything but the newest keypoints); the post half after the join.  (The other
+        assignment, pre half on the second stream, measured 0.233 vs 0.218 ms per fp16 tick;
+        the pre half is only partly hidden either way: 0.187 ms without it, profiles/r04fork/.)"""
         L = _lib.lib()
-        s = torch.cuda.current_stream(self.dev).cuda_stream
-        if not self.zero_copy:
-            self.in_d.copy_(self.in_h, non_blocking=True)
-        # fp16: the preprocess runs inside the stem's row loads (SURVEY 8f.1); fp16x3 / fp32: the
-        # preprocess kernel into the handle's staging, then the forward; the denormalize in the head
-        _lib.check(L.pa_detector_forward_rgbd_px(self._h, self._src[0], self._src[1], self.n,
-                                                 self.sh, self.sw, int(self.bgr), self.near, self.far,
-                                                 self.y.data_ptr(), self.px_d.data_ptr(), s), "forward_rgbd_px")
-        if self.pose_L:
+        cur = torch.cuda.current_stream(self.dev)
+        split = self.pose_L and self.split_pose
+        fw = cur
+        if split:
+            self.side.wait_stream(cur)
+            fw = self.side
+        with torch.cuda.stream(fw):
+            if not self.zero_copy:
+                self.in_d.copy_(self.in_h, non_blocking=True)
+            # fp16: the preprocess runs inside the stem's row loads (SURVEY 8f.1); fp16x3 / fp32: the
+            # preprocess kernel into the handle's staging, then the forward; the denormalize in the head
+            _lib.check(L.pa_detector_forward_rgbd_px(self._h, self._src[0], self._src[1], self.n,
+                                                     self.sh, self.sw, int(self.bgr), self.near, self.far,
+                                                     self.y.data_ptr(), self.px_d.data_ptr(), fw.cuda_stream),
+                       "forward_rgbd_px")
+        if split:
+            self._enqueue_pose_pre()
+            cur.wait_stream(self.side)
+            self._enqueue_pose_post()
+        elif self.pose_L:
             self._enqueue_pose()
         self.out_h.copy_(self.out_d, non_blocking=True)  # pixels (+ info, newest poses): one D2H
 
+    def _enqueue_pose_pre(self):
+        pipeline.window_pose_tick_pre(self.traj_args, self.tick_ws, lam=self.gn.lam)
+
+    def _enqueue_pose_post(self):
+        pipeline.window_pose_tick_post(self.traj_args, self.y, self.tick_ws, delta=self.gn.out["delta"],
+                                       info=self.gn.out["info"], newest=self.pose_d)
+
     def _enqueue_pose(self):
         """The pose stage on the current stream, from the keypoints in self.y (HBM-resident window):
-        advance -> linearize -> GN step -> retract, as pa_window_pose_tick's two launches
-        (fused) or the four separate ones (bit-identical; windows above 24 frames)."""
+        advance -> linearize -> GN step -> retract, as pa_window_pose_tick_pre + _post (split),
+        pa_window_pose_tick's two launches (fused) or the four separate ones (bit-identical to
+        the fused form; windows above 24 frames)."""
+        if self.split_pose:
+            self._enqueue_pose_pre()
+            self._enqueue_pose_post()
+            return
         if self.fused_pose:
             pipeline.window_pose_tick(self.traj_args, self.y, lam=self.gn.lam, delta=self.gn.out["delta"],
                                       info=self.gn.out["info"], newest=self.pose_d)
@@ -204,6 +233,11 @@ class StreamingPipeline:
         # pa_window_pose_tick: one workgroup per camera of up to 24 frames, at most one per CU
         self.fused_pose = (Lw <= pipeline.TICK_MAX_L
                            and n <= torch.cuda.get_device_properties(dev).multi_processor_count)
+        # the split tick (pa_window_pose_tick_pre / _post, same limits): everything but the
+        # newest frame's projection factors runs beside the forward, which gets its own stream
+        self.split_pose = self.fused_pose and self._split_pose_req
+        self.tick_ws = pipeline.window_pose_tick_workspace(n, Lw, dev)
+        self.side = torch.cuda.Stream(dev)
 
     def reset_window(self) -> None:
         """Every frame of every camera's window back to the initial state (keypoints 0, no

@@ -15,8 +15,10 @@ trajectory linearize (the reference's three factors, perseus/smoother/factors.py
   * the smoother tracks a pose: 40 ticks of exact keypoints of a known cube trajectory that
     follows the dynamics model, info == 0 on every tick, and the newest pose converges to the
     true one;
-  * the fused pose tick (pa_window_pose_tick, the default for windows <= 24 frames) equals the
-    four separate launches bit for bit.
+  * the fused pose tick (pa_window_pose_tick) equals the four separate launches bit for bit;
+  * the split pose tick (pa_window_pose_tick_pre beside the forward, _post after it: the
+    default for windows <= 24 frames) equals the fused one up to f64 rounding (another
+    elimination order), its first tick's factors bit for bit.
 """
 import numpy as np
 import pytest
@@ -133,8 +135,8 @@ def test_fused_pose_tick_matches_four_launches(model, graph):
     """pa_window_pose_tick (advance + linearize, then GN step + retract: two launches, the
     shipped tick for windows <= 24 frames) against the four separate launches, bit for bit:
     poses, info, the window, every factor output and delta, over ticks that fill the window."""
-    f, s = _pipe(model, graph), _pipe(model, graph)
-    assert f.fused_pose
+    f, s = _pipe(model, graph, split_pose=False), _pipe(model, graph, split_pose=False)
+    assert f.fused_pose and not f.split_pose
     s.fused_pose = False
     truth, _, _ = _truth(3, LW + 3)
     rng = np.random.default_rng(11)
@@ -152,6 +154,39 @@ def test_fused_pose_tick_matches_four_launches(model, graph):
         assert torch.equal(f.gn.out["delta"], s.gn.out["delta"])
     f.close()
     s.close()
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_split_pose_tick_matches_fused(model, graph):
+    """pa_window_pose_tick_pre + _post against pa_window_pose_tick over ticks that fill the
+    window: the same normal equations, eliminated in another order (the newest frame last), so
+    delta agrees to f64 rounding; the keypoints, statuses and the first tick's factor outputs
+    (the newest frame's projections are evaluated in the post half) are bit-identical."""
+    sp, fu = _pipe(model, graph), _pipe(model, graph, split_pose=False)
+    assert sp.split_pose and not fu.split_pose
+    truth, _, _ = _truth(3, LW + 3)
+    rng = np.random.default_rng(11)
+    for k in range(LW + 3):
+        y = _keypoints(truth[k], 0.5, rng)
+        qs, ins = sp.tick_keypoints(y)
+        qf, inf_ = fu.tick_keypoints(y)
+        np.testing.assert_array_equal(ins, inf_)
+        assert (ins == 0).all()
+        np.testing.assert_allclose(qs, qf, rtol=0, atol=1e-12)
+        ws, wf = sp.window_state(), fu.window_state()
+        np.testing.assert_array_equal(ws["y"], wf["y"])
+        for key in ("pose", "vel", "angvel"):
+            np.testing.assert_allclose(ws[key], wf[key], rtol=0, atol=1e-12, err_msg=key)
+        for key, v in sp.lin.items():
+            if isinstance(v, torch.Tensor):
+                if k == 0 or key == "status":
+                    assert torch.equal(v, fu.lin[key]), (k, key)
+                else:  # the windows differ by the previous steps' rounding
+                    torch.testing.assert_close(v, fu.lin[key], rtol=1e-9, atol=1e-12, msg=f"{k} {key}")
+        ds, df = sp.gn.out["delta"], fu.gn.out["delta"]
+        assert (ds - df).abs().max().item() <= 1e-9 * df.abs().max().item(), k
+    sp.close()
+    fu.close()
 
 
 def _whiten(ref):
@@ -296,9 +331,14 @@ def test_fused_pose_tick_limits(model):
 
     p0, v0, w0 = _init()
     p = StreamingPipeline(model, graph=True, pose_window=30, init_pose=p0, init_vel=v0, init_angvel=w0, **SIG)
-    assert not p.fused_pose
+    assert not p.fused_pose and not p.split_pose
     with pytest.raises(_lib.PerseusError, match="L 30"):
         pipeline.window_pose_tick(p.traj_args, p.y, lam=1e-2, delta=p.gn.out["delta"], info=p.gn.out["info"])
+    ws = torch.empty(1 << 22, dtype=torch.uint8, device=p.dev)
+    with pytest.raises(_lib.PerseusError, match="L 30"):
+        pipeline.window_pose_tick_pre(p.traj_args, ws, lam=1e-2)
+    with pytest.raises(_lib.PerseusError, match="L 30"):
+        pipeline.window_pose_tick_post(p.traj_args, p.y, ws, delta=p.gn.out["delta"], info=p.gn.out["info"])
     truth, _, _ = _truth(3, 3)
     for k in range(3):
         _, info = p.tick_keypoints(_keypoints(truth[k]))
