@@ -326,17 +326,20 @@ def trajset_leg(model, x, args, dev, world, rank, reps=3):
             "timing": f"wall clock, barrier + synchronize, max over ranks, median of {reps}"}
 
 
-def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pose", "pose_parity", "pixels"),
-                  zero_copy=None):
+def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24,
+                  modes=("pose", "pose_parity", "pose_ahead", "pose_parity_ahead", "pixels"), zero_copy=None):
     """configs[4]: 3 x 720p RGBD cameras paced at `hz`, one StreamingPipeline tick per
     camera period (pinned host staging of the centre crops, one hipGraph replay: H2D,
     fused-preprocess forward at B = cams, denormalize, D2H pixels; mode "pose" adds the
     pose stage over a `window`-frame fixed-lag window per camera: advance, linearize the
     reference's factors, one GN step, retract, D2H poses; "pose_parity" is the same tick
     with the detector in fp16x3, the mode that meets north_star's 1e-3 px, in its latency
-    mode).  Latency = host time from the start of staging to results on the host, p50 / p99
-    / max over `ticks` paced ticks (mode "pixels": ticks // 3); device_ms = one replay
-    between HIP events on the pipeline's stream (20 back to back)."""
+    mode; "_ahead": the same ticks with the next tick's pre half run right after the results,
+    in the gap before the next frames, StreamingPipeline(pre_ahead=True)).  Latency = host
+    time from the start of staging to results on the host, p50 / p99 / max over `ticks` paced
+    ticks (mode "pixels": ticks // 3); device_ms = one tick's device work between HIP events
+    on the pipeline's stream (20 back to back; "_ahead": including the next tick's pre half),
+    latency_path_ms ("_ahead") = from a tick's start to its results (median of 20 ticks)."""
     import numpy as np
     import torch
 
@@ -344,7 +347,7 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pos
     from perseus_amd.streaming import StreamingPipeline
 
     parity = None
-    if "pose_parity" in modes:  # the same weights in the parity-grade precision
+    if any(m.startswith("pose_parity") for m in modes):  # the same weights in the parity-grade precision
         parity = KeypointCNN(num_channels=4, precision="fp16x3")
         parity.load_state_dict(model.state_dict())
 
@@ -356,8 +359,9 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pos
            "unit": "ms", "timing": "host time from staging start to results on the host, paced ticks"}
     for mode in modes:
         kw = dict(pose_window=window, proj_sigma=40.0) if mode.startswith("pose") else {}
-        pipe = StreamingPipeline(parity if mode == "pose_parity" else model, n_cams=cams, graph=True, host_crop=True,
-                                 device=dev, zero_copy=zero_copy, **kw)
+        ahead = mode.endswith("_ahead")
+        pipe = StreamingPipeline(parity if mode.startswith("pose_parity") else model, n_cams=cams, graph=True,
+                                 host_crop=True, device=dev, zero_copy=zero_copy, pre_ahead=ahead, **kw)
         for i in range(10):
             pipe(rgbs[i % n_src], deps[i % n_src])
         n = ticks if mode.startswith("pose") else max(ticks // 3, 30)
@@ -377,17 +381,28 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24, modes=("pos
         with torch.cuda.stream(s):
             e0.record(s)
             for _ in range(20):
-                pipe.graph.replay()
+                pipe.replay()
             e1.record(s)
         s.synchronize()
         r = {"ticks": n, "p50_ms": round(float(np.percentile(lat, 50)), 4),
              "p99_ms": round(float(np.percentile(lat, 99)), 4), "max_ms": round(float(lat.max()), 4),
              "device_ms_per_tick": round(e0.elapsed_time(e1) / 20, 4)}
+        if ahead:
+            path = []
+            for _ in range(20):
+                with torch.cuda.stream(s):
+                    e0.record(s)
+                    pipe.replay()
+                s.synchronize()
+                path.append(e0.elapsed_time(pipe._done))
+            r["latency_path_ms"] = round(float(np.median(path)), 4)
         if mode.startswith("pose"):
             r["window_frames"] = window
             r["precision"] = pipe.model.precision
             r["stage"] = ("forward_rgbd_px (latency mode) + " +
-                          ("pa_window_pose_tick (advance + linearize, GN step + retract: two launches)"
+                          ("pa_window_pose_tick_pre (next tick's, after the results) + _post" if pipe.pre_ahead else
+                           "pa_window_pose_tick_pre (beside the forward) + _post" if pipe.split_pose else
+                           "pa_window_pose_tick (advance + linearize, GN step + retract: two launches)"
                            if getattr(pipe, "fused_pose", False) else
                            "pa_window_advance_n + pa_trajectory_linearize + pa_trajectory_gn_step (delta + info) + "
                            "pa_window_retract_newest"))

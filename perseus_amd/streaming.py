@@ -53,7 +53,7 @@ class StreamingPipeline:
                  pose_window: int = 0, K=None, corners=None, dt: float = 1.0 / 30.0, vel_frame: str = "world",
                  proj_sigma: float = 1.0, dyn_sigma: float = 0.1, cv_sigma: float = 0.1, lam: float = 1e-2,
                  init_pose=None, init_vel=None, init_angvel=None, split_k: bool = True,
-                 zero_copy: bool | None = None, split_pose: bool = True):
+                 zero_copy: bool | None = None, split_pose: bool = True, pre_ahead: bool = False):
         if not torch.cuda.is_available():
             raise RuntimeError("StreamingPipeline needs a ROCm GPU (no CPU fallback)")
         cam_K = K  # (the name K is the keypoint count below)
@@ -127,21 +127,31 @@ class StreamingPipeline:
             raise ValueError("StreamingPipeline feeds RGBD (num_channels=4)")
         self.pose_L = int(pose_window)
         self._split_pose_req = bool(split_pose)
-        self.fused_pose = self.split_pose = False
+        self._pre_ahead_req = bool(pre_ahead)
+        self.fused_pose = self.split_pose = self.pre_ahead = False
         if self.pose_L:
             self._init_pose_stage(cam_K, corners, dt, vel_frame, proj_sigma, dyn_sigma, cv_sigma, lam, init_pose,
                                   init_vel, init_angvel)
         self.graph = None
+        self.pre_graph = None
         with torch.cuda.stream(self.stream):
+            if self.pre_ahead:
+                self._enqueue_pose_pre()
             self._enqueue()  # eager warm-up (also builds the kernels' first-launch state)
         self.stream.synchronize()
         if self.pose_L:
-            self.reset_window()  # the warm-up tick advanced it
+            self.reset_window()  # the warm-up tick advanced it (pre_ahead: and prepares the next tick)
         if graph:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=self.stream):
                 self._enqueue()
             self.graph = g
+            if self.pre_ahead:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=self.stream):
+                    self._enqueue_pose_pre()
+                self.pre_graph = g
+        self._done = torch.cuda.Event(enable_timing=True)  # (timed: the bench's latency path)
 
     def _enqueue(self):
         """H2D, preprocess + forward + denormalize, [pose stage], D2H on the current stream.
@@ -151,7 +161,7 @@ class StreamingPipeline:
         the pre half is only partly hidden either way: 0.187 ms without it, profiles/r04fork/.)"""
         L = _lib.lib()
         cur = torch.cuda.current_stream(self.dev)
-        split = self.pose_L and self.split_pose
+        split = self.pose_L and self.split_pose and not self.pre_ahead
         fw = cur
         if split:
             self.side.wait_stream(cur)
@@ -170,7 +180,7 @@ class StreamingPipeline:
             cur.wait_stream(self.side)
             self._enqueue_pose_post()
         elif self.pose_L:
-            self._enqueue_pose()
+            self._enqueue_pose()  # (pre_ahead: the post half alone)
         self.out_h.copy_(self.out_d, non_blocking=True)  # pixels (+ info, newest poses): one D2H
 
     def _enqueue_pose_pre(self):
@@ -186,7 +196,8 @@ class StreamingPipeline:
         pa_window_pose_tick's two launches (fused) or the four separate ones (bit-identical to
         the fused form; windows above 24 frames)."""
         if self.split_pose:
-            self._enqueue_pose_pre()
+            if not self.pre_ahead:
+                self._enqueue_pose_pre()
             self._enqueue_pose_post()
             return
         if self.fused_pose:
@@ -236,6 +247,10 @@ class StreamingPipeline:
         # the split tick (pa_window_pose_tick_pre / _post, same limits): everything but the
         # newest frame's projection factors runs beside the forward, which gets its own stream
         self.split_pose = self.fused_pose and self._split_pose_req
+        # pre_ahead: the pre half of tick k + 1 runs right after tick k's results are on the host
+        # (in the gap before the next camera frames), so a tick's latency path is H2D, forward,
+        # post half, D2H.  The window and factor outputs then already hold the next tick's advance.
+        self.pre_ahead = self.split_pose and self._pre_ahead_req
         self.tick_ws = pipeline.window_pose_tick_workspace(n, Lw, dev)
         self.side = torch.cuda.Stream(dev)
 
@@ -248,10 +263,13 @@ class StreamingPipeline:
             for k in ("pose", "vel", "angvel"):
                 self.win[k].copy_(torch.as_tensor(self._init[k], device=self.dev)[:, None, :]
                                   .expand_as(self.win[k]))
+            if self.pre_ahead:  # the next tick's pre half, from the reset window
+                self._enqueue_pose_pre()
         self.stream.synchronize()
 
     def window_state(self) -> dict:
-        """Host copies of the window (y, pose, vel, angvel) after the last tick."""
+        """Host copies of the window (y, pose, vel, angvel) after the last tick (pre_ahead: after
+        the next tick's advance, whose newest keypoints are not in yet)."""
         self.stream.synchronize()
         return {k: v.cpu().numpy().copy() for k, v in self.win.items()}
 
@@ -268,14 +286,31 @@ class StreamingPipeline:
             self.rgb_h.numpy()[:] = rgb
             self.depth_h.numpy()[:] = depth
 
+    def replay(self) -> None:
+        """One tick's device work on the current stream, no wait (pre_ahead: then the next
+        tick's pre half, after self._done is recorded)."""
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._enqueue()
+        if self.pre_ahead:
+            self._done.record()
+            self._pre()
+
+    def _pre(self):
+        if self.pre_graph is not None:
+            self.pre_graph.replay()
+        else:
+            self._enqueue_pose_pre()
+
     def run(self) -> np.ndarray:
         """Process the staged tick; returns a copy of the (n, K, 2) pixel coordinates."""
         with torch.cuda.stream(self.stream):  # replay() launches on the current stream
-            if self.graph is not None:
-                self.graph.replay()
-            else:
-                self._enqueue()
-        self.stream.synchronize()
+            self.replay()
+        if self.pre_ahead:
+            self._done.synchronize()  # the results; the next tick's pre half keeps running
+        else:
+            self.stream.synchronize()
         return self.px_h.numpy().copy()
 
     def __call__(self, rgb: np.ndarray, depth: np.ndarray) -> np.ndarray:
@@ -314,13 +349,17 @@ class StreamingPipeline:
                 self.pose_graph.replay()
             else:
                 enqueue()
-        self.stream.synchronize()
+            if self.pre_ahead:
+                self._done.record()
+                self._pre()
+        (self._done if self.pre_ahead else self.stream).synchronize()
         return self.pose_h.numpy().copy(), self.info_h.numpy().copy()
 
     def close(self) -> None:
         """Drop the graphs, then the handle they captured."""
         self.graph = None
         self.pose_graph = None
+        self.pre_graph = None
         if getattr(self, "_h", None) is not None:
             torch.cuda.synchronize(self.dev)
             _lib.lib().pa_detector_destroy(self._h)

@@ -18,7 +18,8 @@ trajectory linearize (the reference's three factors, perseus/smoother/factors.py
   * the fused pose tick (pa_window_pose_tick) equals the four separate launches bit for bit;
   * the split pose tick (pa_window_pose_tick_pre beside the forward, _post after it: the
     default for windows <= 24 frames) equals the fused one up to f64 rounding (another
-    elimination order), its first tick's factors bit for bit.
+    elimination order), its first tick's factors bit for bit; with pre_ahead (the next tick's
+    pre half right after the results) bit for bit the split tick.
 """
 import numpy as np
 import pytest
@@ -187,6 +188,32 @@ def test_split_pose_tick_matches_fused(model, graph):
         assert (ds - df).abs().max().item() <= 1e-9 * df.abs().max().item(), k
     sp.close()
     fu.close()
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_pre_ahead_matches_split(model, graph):
+    """StreamingPipeline(pre_ahead=True): the next tick's pre half runs right after a tick's
+    results (off the latency path).  The same kernels on the same data, so pixels, poses and
+    info are bit for bit the split tick's, over camera ticks, keypoint ticks and a reset."""
+    a, b = _pipe(model, graph), _pipe(model, graph, pre_ahead=True)
+    assert b.pre_ahead and not a.pre_ahead
+    truth, _, _ = _truth(3, 6)
+    for seed in range(1, 4):
+        rgb, d = _frames(seed)
+        for x, y_ in zip(a.tick(rgb, d), b.tick(rgb, d)):
+            np.testing.assert_array_equal(x, y_)
+    for k in range(3):
+        y = _keypoints(truth[k])
+        for x, y_ in zip(a.tick_keypoints(y), b.tick_keypoints(y)):
+            np.testing.assert_array_equal(x, y_)
+    a.reset_window()
+    b.reset_window()
+    for k in range(3, 6):
+        y = _keypoints(truth[k])
+        for x, y_ in zip(a.tick_keypoints(y), b.tick_keypoints(y)):
+            np.testing.assert_array_equal(x, y_)
+    a.close()
+    b.close()
 
 
 def _whiten(ref):
