@@ -1127,10 +1127,12 @@ struct GnCrLds {
   static constexpr int POOL = PAIR ? W * SLAB : (POST > STG ? POST : STG);
 };
 
-// The split streaming tick (pa_window_pose_tick_pre / _post): per trajectory, the reduced
-// system the pre half leaves for the post half in the workspace a.ws (doubles): PM | QM | z
-// of every eliminated frame (the pool, L x FR), the root's S | b, the failure word
-constexpr int GN_TICK_WSD = GN_CR_LMAX * (2 * gn::NB + gn::NV) + gn::NB + gn::NV + 2;
+// The split streaming tick (pa_window_pose_tick_pre / _post): per trajectory, what the pre
+// half leaves for the post half in the workspace a.ws (doubles): per frame B_l | a_l (the
+// back substitution run on the root's delta as an unknown: delta_l = a_l + B_l delta_root),
+// the root's S | b, the failure word
+constexpr int GN_TICK_FRD = gn::NB + gn::NV;
+constexpr int GN_TICK_WSD = GN_CR_LMAX * GN_TICK_FRD + gn::NB + gn::NV + 2;
 
 // the level lists: frames active at each level, the parity of the eliminated positions
 // (pe), the level count.  Shipped order: n even -> the odd positions, n odd -> the even ones
@@ -1314,12 +1316,52 @@ __device__ __forceinline__ void gn_cr_run(const GnArgs& a, int t, double (*fb)[2
     __syncthreads();
     if (wv == 0) gn_stamp(a, t, 11 + 2 * lv);
   }
-  if constexpr (ROOT) {  // the reduced system to the workspace (the root is frame L - 1)
+  if constexpr (ROOT) {
+    // the root (frame L - 1) S | b and the failure word to the workspace, then the back
+    // substitution with delta_root unknown: delta_l = a_l + B_l delta_root, B_root = I, a_root = 0,
+    //   B_i = -(PM_i^T B_p + QM_i^T B_q),  a_i = z_i - PM_i^T a_p - QM_i^T a_q
+    // level by level in reverse (the products on the f64 matrix cores), into fb[l] (its S and C
+    // are dead): B_l | a_l, then to the workspace
+    constexpr int FD = GN_TICK_FRD;
     double* w = a.ws + (size_t)t * GN_TICK_WSD;
-    for (int e = threadIdx.x; e < L * FR / 2; e += 64 * W)
-      reinterpret_cast<gn_d2*>(w)[e] = reinterpret_cast<const gn_d2*>(pool)[e];
-    for (int e = threadIdx.x; e < NB + NV; e += 64 * W) w[LM * FR + e] = e < NB ? fb[L - 1][e] : fb[L - 1][NB + e];
-    if (threadIdx.x == 0) reinterpret_cast<int*>(w + LM * FR + NB + NV)[0] = fail == NOFAIL ? 0 : fail;
+    const int rt = L - 1;
+    for (int e = threadIdx.x; e < NB + NV; e += 64 * W) w[LM * FD + e] = e < NB ? fb[rt][e] : fb[rt][NB + e];
+    if (threadIdx.x == 0) reinterpret_cast<int*>(w + LM * FD + NB + NV)[0] = fail == NOFAIL ? 0 : fail;
+    if (fail != NOFAIL) return;  // (uniform: read after the last level's barrier)
+    __syncthreads();  // every read of the root's S | b is done
+    for (int e = threadIdx.x; e < FD; e += 64 * W) fb[rt][e] = (e < NB && e % (NV + 1) == 0) ? 1.0 : 0.0;
+    __syncthreads();
+    for (lv = nlev - 1; lv >= 0; --lv) {
+      const int n = lcnt[lv], pe = lpe[lv];
+      const int ne = pe ? n / 2 : (n + 1) / 2;
+      for (int e = wv; e < ne; e += W) {
+        const int pos = 2 * e + pe;
+        const int fi = lst[lv][pos];
+        const int fp = pos > 0 ? lst[lv][pos - 1] : -1, fq = pos + 1 < n ? lst[lv][pos + 1] : -1;
+        const double* o = fr(fi);
+        gn_d4 acc = {0.0, 0.0, 0.0, 0.0};
+        if (fp >= 0) acc = gn_mm_acc<true, false>(o, fb[fp], acc);
+        if (fq >= 0) acc = gn_mm_acc<true, false>(o + NB, fb[fq], acc);
+        double av = 0.0;
+        if (i < NV) {
+          double d0 = o[2 * NB + i], d1 = 0.0;
+          if (fp >= 0)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) d0 -= o[k * NV + i] * fb[fp][NB + k];
+          if (fq >= 0)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) d1 += o[NB + k * NV + i] * fb[fq][NB + k];
+          av = d0 - d1;
+        }
+        gn_mm_store(fb[fi], acc, -1.0);  // (fb[fi] is this wave's alone; nothing above reads it)
+        if (i < NV) fb[fi][NB + i] = av;
+      }
+      __syncthreads();
+    }
+    for (int e = threadIdx.x; e < L * FD / 2; e += 64 * W) {
+      const int l = e / (FD / 2), c = e - l * (FD / 2);
+      reinterpret_cast<gn_d2*>(w + l * FD)[c] = reinterpret_cast<const gn_d2*>(fb[l])[c];
+    }
     return;
   }
   if (fail == NOFAIL && wv == 0) {  // the last active frame: delta = S^-1 b (over its S block)
@@ -1484,27 +1526,32 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void pose_tick_post_kernel(pa_traj
                                                                           const double* __restrict__ ws, double* delta,
                                                                           int32_t* info, double* newest) {
   using namespace gn;
-  constexpr int LM = GN_CR_LMAX, W = GN_CR_W, FR = 2 * NB + NV, KP = 2 * GN_KMAX;
-  __shared__ __attribute__((aligned(16))) double pool[LM * FR];  // PM | QM | z per eliminated frame
-  __shared__ __attribute__((aligned(16))) double dl[LM][NV];     // delta per frame
-  __shared__ __attribute__((aligned(16))) double sr[NB + NV];    // the root's S | b
-  __shared__ __attribute__((aligned(16))) double jt[7][KP];      // newest frame: Jp^T (6 x 2K) | rp
+  constexpr int KP = 2 * GN_KMAX, FD = GN_TICK_FRD, LM = GN_CR_LMAX;
+  __shared__ __attribute__((aligned(16))) double dl[LM][NV];   // delta per frame
+  __shared__ __attribute__((aligned(16))) double sr[NB + NV];  // the root's S | b
+  __shared__ __attribute__((aligned(16))) double jt[7][KP];    // newest frame: Jp^T (6 x 2K) | rp
   __shared__ __attribute__((aligned(16))) GnChainLds C;
-  __shared__ signed char lst[8][LM];
-  __shared__ int lcnt[8], lpe[8];
-  __shared__ int nlev_s, fail_s;
+  __shared__ int fail_s;
   const int t = blockIdx.x, L = ta.L, K = ta.n_kp, ny = 2 * K;
   const int wv = threadIdx.x >> 6, i = threadIdx.x & 63;
   const long f0 = (long)t * L, fn = f0 + L - 1;
   const double* w = ws + (size_t)t * GN_TICK_WSD;
-  // the pre half's reduced system -> LDS (every load in flight before the projections)
-  for (int e = threadIdx.x; e < L * FR / 2; e += 64 * W)
-    reinterpret_cast<gn_d2*>(pool)[e] = reinterpret_cast<const gn_d2*>(w)[e];
-  for (int e = threadIdx.x; e < NB + NV; e += 64 * W) sr[e] = w[LM * FR + e];
-  if (threadIdx.x == 0) {
-    nlev_s = gn_cr_lists<false, true>(L, lst, lcnt, lpe);
-    fail_s = reinterpret_cast<const int*>(w + LM * FR + NB + NV)[0];
+  // thread (l, r) < L x 12: row r of B_l and a_l[r], loaded first (in flight with the rest)
+  const int tl = (int)threadIdx.x / NV, tr = (int)threadIdx.x - tl * NV;
+  const bool brow = tl < L;
+  double bv[NV], av = 0.0;
+  if (brow) {
+    const double* src = w + tl * FD;
+#pragma unroll
+    for (int k = 0; k < NV; k += 2) {
+      const gn_d2 v = *reinterpret_cast<const gn_d2*>(src + tr * NV + k);
+      bv[k] = v[0];
+      bv[k + 1] = v[1];
+    }
+    av = src[NB + tr];
   }
+  for (int e = threadIdx.x; e < NB + NV; e += 64 * GN_CR_W) sr[e] = w[LM * FD + e];
+  if (threadIdx.x == 0) fail_s = reinterpret_cast<const int*>(w + LM * FD + NB + NV)[0];
   double s = 0.0;  // wave 0, lane o < 42: entry o of [Jp^T Jp | Jp^T rp] (6 x 7, row-major)
   if (wv == 0) {
     // y_new lands (pa_window_advance's last step) and frame L - 1's projection factors:
@@ -1549,17 +1596,16 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void pose_tick_post_kernel(pa_traj
       for (int q = 0; q < ny; ++q) s += jt[ra][q] * jt[cb][q];
     }
   }
-  __syncthreads();  // the reduced system, the level lists
-  const int nlev = nlev_s;
-  const bool act = i < 36;
-  const int ii = act ? i : 35;
-  const int r = ii / 3, c0 = 4 * (ii - 3 * (ii / 3));
+  __syncthreads();  // the root's S | b, the failure word
   if (wv == 0) {
     // the newest frame's projections into the root (S += Jp^T Jp on the pose block, b -= Jp^T rp)
     if (i < 36) sr[(i / 6) * NV + i - 6 * (i / 6)] += s;
     else if (i < 42) sr[NB + i - 36] -= s;
     wave_order();
     if (fail_s == 0) {  // delta_root = S^-1 b
+      const bool act = i < 36;
+      const int ii = act ? i : 35;
+      const int r = ii / 3, c0 = 4 * (ii - 3 * (ii / 3));
       double sv[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) sv[c] = sr[r * NV + c0 + c];
@@ -1575,36 +1621,25 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void pose_tick_post_kernel(pa_traj
   }
   __syncthreads();
   const int inf = fail_s;
-  if (!inf) {
-    for (int lv = nlev - 1; lv >= 0; --lv) {  // gn_cr_run's back substitution
-      const int n = lcnt[lv], pe = lpe[lv];
-      const int ne = pe ? n / 2 : (n + 1) / 2;
-      for (int e = wv; e < ne; e += W) {
-        const int pos = 2 * e + pe;
-        const int fi = lst[lv][pos];
-        const int fp = pos > 0 ? lst[lv][pos - 1] : -1, fq = pos + 1 < n ? lst[lv][pos + 1] : -1;
-        const double* o = pool + fi * FR;
-        if (i < NV) {
-          double d0 = o[2 * NB + i], d1 = 0.0;
-          if (fp >= 0)
+  // every frame at once: delta_l = a_l + B_l delta_root
+  double dv = NAN;
+  if (brow && !inf) {
+    double d0 = av, d1 = 0.0;
 #pragma unroll
-            for (int k = 0; k < NV; ++k) d0 -= o[k * NV + i] * dl[fp][k];
-          if (fq >= 0)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) d1 += o[NB + k * NV + i] * dl[fq][k];
-          dl[fi][i] = d0 - d1;
-        }
-      }
-      __syncthreads();
+    for (int k = 0; k < NV; k += 2) {
+      d0 += bv[k] * dl[L - 1][k];
+      d1 += bv[k + 1] * dl[L - 1][k + 1];
     }
+    dv = d0 + d1;
   }
-  double* dt = delta + (size_t)f0 * NV;
-  for (int e = threadIdx.x; e < L * NV; e += 64 * W) {
-    const int l = e / NV;
-    dt[e] = inf ? NAN : dl[l][e - l * NV];
+  __syncthreads();  // every read of delta_root is done
+  if (brow) {
+    dl[tl][tr] = dv;
+    delta[(size_t)f0 * NV + threadIdx.x] = dv;
   }
   if (threadIdx.x == 0) info[t] = inf;
-  if ((int)threadIdx.x < L)  // (delta from LDS: the back substitution's last barrier is behind it)
+  __syncthreads();
+  if ((int)threadIdx.x < L)
     window_retract_frame(f0 + threadIdx.x, L, dl[threadIdx.x], inf == 0, const_cast<double*>(ta.pose),
                          const_cast<double*>(ta.angvel), const_cast<double*>(ta.vel), newest);
 }
