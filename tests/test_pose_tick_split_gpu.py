@@ -1,0 +1,74 @@
+"""pa_window_pose_tick_pre + _post (the split streaming tick, csrc/gn.hip) against
+pa_window_pose_tick (the fused tick, itself bit-identical to the four separate calls) at every
+level structure of the ROOT-order cyclic reduction: L = 2 .. 24 (even and odd level counts,
+the n = 3 -> 2 -> 1 tail), n_kp = 8 (the RP = 34 instance) and 16 (the general one), windows
+whose first frames are unmeasured (nvalid = L - 2: status-2 rows).  Same inputs, three ticks
+each: info equal, the split delta solves the damped normal equations of its factors (the dense
+oracle's backward error, oracle/gn_ref.py) and agrees with the fused delta within
+max(1e-9, 100 cond eps) (another elimination order in f64; the random windows are not all well
+conditioned), statuses and the window's keypoints equal."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gn_ref as G
+from perseus_amd import pipeline, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(L, nk, seed):
+    T = 3
+    dev = torch.device("cuda", 0)
+    tr = synth.synthetic_trajectories(seed, T, L, n_kp=nk)
+    nvalid = torch.full((T,), max(L - 2, 1), dtype=torch.int32, device=dev)
+    y = torch.as_tensor(tr["y"], device=dev)
+    corners = np.asarray(tr["corners"])
+    if len(corners) < nk:  # (the synthetic set has the 8 cube corners: 8 more inside the cube)
+        corners = np.concatenate([corners, 0.5 * corners])[:nk]
+    a, lin = pipeline.prepare_trajectories(y, tr["poses"], tr["vels"], tr["angvels"], corners, tr["K"], T=T,
+                                           L=L, dt=1 / 30, proj_sigmas=[2.0, 2.0], dyn_sigmas=[0.1] * 6,
+                                           cv_sigmas=[0.5] * 3, nvalid=nvalid)
+    out = dict(delta=torch.zeros((T * L, 12), dtype=torch.float64, device=dev),
+               info=torch.zeros(T, dtype=torch.int32, device=dev),
+               newest=torch.zeros((T, 12), dtype=torch.float64, device=dev))
+    return a, lin, out, tr
+
+
+@pytest.mark.parametrize("nk", [8, 16])
+@pytest.mark.parametrize("L", [2, 3, 4, 5, 7, 12, 13, 23, 24])
+def test_split_tick_matches_fused(L, nk):
+    fa, flin, fout, tr = _setup(L, nk, 100 + L)
+    sa, slin, sout, _ = _setup(L, nk, 100 + L)
+    ws = pipeline.window_pose_tick_workspace(3, L, torch.device("cuda", 0))
+    rng = np.random.default_rng(L)
+    for k in range(3):
+        y_new = torch.as_tensor((tr["y"][:3] + 0.01 * rng.standard_normal(tr["y"][:3].shape)).astype(np.float32),
+                                device="cuda").contiguous()
+        pipeline.window_pose_tick(fa, y_new, lam=1e-2, **fout)
+        pipeline.window_pose_tick_pre(sa, ws, lam=1e-2)
+        pipeline.window_pose_tick_post(sa, y_new, ws, **sout)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(sout["info"].cpu().numpy(), fout["info"].cpu().numpy())
+        assert (fout["info"] == 0).all()
+        # the split step solves the damped normal equations of its own factors (dense oracle,
+        # backward error), and agrees with the fused step (a wrong elimination order or a lost
+        # factor shows as O(delta))
+        lin = {kk: (v.transpose(1, 2) if kk.startswith("j_") else v).cpu().numpy() for kk, v in slin.items()
+               if isinstance(v, torch.Tensor)}
+        H, g, _ = G.gn_step(lin, 3, L, nk, 1e-2)
+        ds = sout["delta"].cpu().numpy().reshape(3, -1)
+        df = fout["delta"].cpu().numpy().reshape(3, -1)
+        for t in range(3):
+            M = H[t] + 1e-2 * np.eye(H.shape[1])
+            res = M @ ds[t] + g[t]
+            assert np.abs(res).max() <= 1e-10 * (np.abs(M).max() * np.abs(ds[t]).max() + np.abs(g[t]).max()), (k, t)
+            # forward agreement within the f64 bound for the conditioning of this system
+            tol = max(1e-9, 100 * np.linalg.cond(M) * np.finfo(np.float64).eps)
+            assert np.abs(ds[t] - df[t]).max() <= tol * np.abs(df[t]).max(), (k, t)
+        assert torch.equal(slin["status"], flin["status"]), (k, L)
+        assert torch.equal(slin["_keep"][0], flin["_keep"][0])  # the window's keypoints
+        # the fused tick ran on its own window, which has drifted by the earlier ticks' rounding:
+        # from here on the split tick continues from the fused tick's state
+        for i in (1, 2, 3):  # pose, vel, angvel of the window
+            slin["_keep"][i].copy_(flin["_keep"][i])
