@@ -327,7 +327,8 @@ def trajset_leg(model, x, args, dev, world, rank, reps=3):
 
 
 def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24,
-                  modes=("pose", "pose_parity", "pose_ahead", "pose_parity_ahead", "pixels"), zero_copy=None):
+                  modes=("pose", "pose_parity", "pose_ahead", "pose_parity_ahead", "pixels"), zero_copy=None,
+                  zero_copy_out=True):
     """configs[4]: 3 x 720p RGBD cameras paced at `hz`, one StreamingPipeline tick per
     camera period (pinned host staging of the centre crops, one hipGraph replay: H2D,
     fused-preprocess forward at B = cams, denormalize, D2H pixels; mode "pose" adds the
@@ -361,7 +362,8 @@ def streaming_leg(model, dev, ticks=300, hz=30.0, cams=3, window=24,
         kw = dict(pose_window=window, proj_sigma=40.0) if mode.startswith("pose") else {}
         ahead = mode.endswith("_ahead")
         pipe = StreamingPipeline(parity if mode.startswith("pose_parity") else model, n_cams=cams, graph=True,
-                                 host_crop=True, device=dev, zero_copy=zero_copy, pre_ahead=ahead, **kw)
+                                 host_crop=True, device=dev, zero_copy=zero_copy, pre_ahead=ahead,
+                                 zero_copy_out=zero_copy_out, **kw)
         for i in range(10):
             pipe(rgbs[i % n_src], deps[i % n_src])
         n = ticks if mode.startswith("pose") else max(ticks // 3, 30)

@@ -147,9 +147,9 @@ def check(rc: int, what: str = "") -> int:
 
 
 def ptr(t) -> int | None:
-    """Device pointer of a torch tensor (None for None)."""
-    if t is None:
-        return None
+    """Device pointer of a torch tensor (None for None; an int is taken as a device address)."""
+    if t is None or isinstance(t, int):
+        return t
     return t.data_ptr()
 
 

@@ -244,11 +244,12 @@ def window_pose_tick_pre(args, ws: torch.Tensor, *, lam: float) -> None:
 def window_pose_tick_post(args, y_new: torch.Tensor, ws: torch.Tensor, *, delta: torch.Tensor, info: torch.Tensor,
                           newest: torch.Tensor | None = None) -> None:
     """pa_window_pose_tick_post on the device's current stream: y_new lands, the newest frame's
-    projection factors join the reduced system, solve (delta, info), retract (newest)."""
+    projection factors join the reduced system, solve (delta, info), retract (newest).  info /
+    newest: tensors or device addresses (e.g. of mapped pinned host memory)."""
     dev = y_new.device
     with torch.cuda.device(dev):
         _lib.check(_lib.lib().pa_window_pose_tick_post(C.byref(args), y_new.data_ptr(), ws.data_ptr(), ws.numel(),
-                                                       delta.data_ptr(), info.data_ptr(), _lib.ptr(newest),
+                                                       delta.data_ptr(), _lib.ptr(info), _lib.ptr(newest),
                                                        _lib.stream_of(dev)), "pa_window_pose_tick_post")
 
 

@@ -53,7 +53,8 @@ class StreamingPipeline:
                  pose_window: int = 0, K=None, corners=None, dt: float = 1.0 / 30.0, vel_frame: str = "world",
                  proj_sigma: float = 1.0, dyn_sigma: float = 0.1, cv_sigma: float = 0.1, lam: float = 1e-2,
                  init_pose=None, init_vel=None, init_angvel=None, split_k: bool = True,
-                 zero_copy: bool | None = None, split_pose: bool = True, pre_ahead: bool = False):
+                 zero_copy: bool | None = None, split_pose: bool = True, pre_ahead: bool = False,
+                 zero_copy_out: bool = True):
         if not torch.cuda.is_available():
             raise RuntimeError("StreamingPipeline needs a ROCm GPU (no CPU fallback)")
         cam_K = K  # (the name K is the keypoint count below)
@@ -81,6 +82,7 @@ class StreamingPipeline:
             raise ValueError(f"staging: {n} x {sh} x {sw} RGB bytes not 4-aligned for the depth block")
         nin = nr + n * sh * sw * 4
         self._po = ((n * K * 2 + n) * 4 + 7) // 8 * 8
+        self._px_bytes = n * K * 8
         nout = self._po + n * 12 * 8
         self.in_h = torch.empty(nin, dtype=torch.uint8).pin_memory()
         self.in_d = torch.empty(nin, dtype=torch.uint8, device=self.dev)
@@ -106,6 +108,17 @@ class StreamingPipeline:
             _lib.check(_lib.lib().pa_host_device_pointer(C.c_void_p(self.in_h.data_ptr()), C.byref(dp)),
                        "host_device_pointer")
             self._src = (dp.value, dp.value + nr)
+        # zero_copy_out: the head writes the pixels, and the split tick's post half info and the
+        # newest poses, straight into the pinned output block over PCIe (a few hundred bytes), so
+        # the tick has no D2H copy; the fused / four-launch pose stages keep the copy
+        self._zc_out = bool(zero_copy_out)
+        self._px_out = self.px_d.data_ptr()
+        if self._zc_out:
+            dp = C.c_void_p()
+            _lib.check(_lib.lib().pa_host_device_pointer(C.c_void_p(self.out_h.data_ptr()), C.byref(dp)),
+                       "host_device_pointer")
+            self._out_dev = dp.value
+            self._px_out = dp.value
         self.y = torch.empty((n, 2 * K), dtype=torch.float32, device=self.dev)
         self.y_h = torch.empty((n, 2 * K), dtype=torch.float32).pin_memory()  # tick_keypoints' input
         self.pose_graph = None
@@ -173,7 +186,7 @@ class StreamingPipeline:
             # preprocess kernel into the handle's staging, then the forward; the denormalize in the head
             _lib.check(L.pa_detector_forward_rgbd_px(self._h, self._src[0], self._src[1], self.n,
                                                      self.sh, self.sw, int(self.bgr), self.near, self.far,
-                                                     self.y.data_ptr(), self.px_d.data_ptr(), fw.cuda_stream),
+                                                     self.y.data_ptr(), self._px_out, fw.cuda_stream),
                        "forward_rgbd_px")
         if split:
             self._enqueue_pose_pre()
@@ -181,14 +194,25 @@ class StreamingPipeline:
             self._enqueue_pose_post()
         elif self.pose_L:
             self._enqueue_pose()  # (pre_ahead: the post half alone)
-        self.out_h.copy_(self.out_d, non_blocking=True)  # pixels (+ info, newest poses): one D2H
+        self._enqueue_out()
+
+    def _enqueue_out(self):
+        """pixels (+ info, newest poses) to the host: one D2H, or nothing (zero_copy_out)."""
+        if not self._zc_out:
+            self.out_h.copy_(self.out_d, non_blocking=True)
+        elif self.pose_L and not self.split_pose:  # the fused / four-launch stages write the device block
+            self.out_h[self._px_bytes:].copy_(self.out_d[self._px_bytes:], non_blocking=True)
 
     def _enqueue_pose_pre(self):
         pipeline.window_pose_tick_pre(self.traj_args, self.tick_ws, lam=self.gn.lam)
 
     def _enqueue_pose_post(self):
-        pipeline.window_pose_tick_post(self.traj_args, self.y, self.tick_ws, delta=self.gn.out["delta"],
-                                       info=self.gn.out["info"], newest=self.pose_d)
+        if self._zc_out:  # info and the newest poses straight into the pinned output block
+            info, newest = self._out_dev + self._px_bytes, self._out_dev + self._po
+        else:
+            info, newest = self.gn.out["info"], self.pose_d
+        pipeline.window_pose_tick_post(self.traj_args, self.y, self.tick_ws, delta=self.gn.out["delta"], info=info,
+                                       newest=newest)
 
     def _enqueue_pose(self):
         """The pose stage on the current stream, from the keypoints in self.y (HBM-resident window):
@@ -337,7 +361,7 @@ class StreamingPipeline:
         def enqueue():
             self.y.copy_(self.y_h, non_blocking=True)
             self._enqueue_pose()
-            self.out_h.copy_(self.out_d, non_blocking=True)
+            self._enqueue_out()
 
         with torch.cuda.stream(self.stream):
             if self.graph is not None:

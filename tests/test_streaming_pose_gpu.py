@@ -216,6 +216,26 @@ def test_pre_ahead_matches_split(model, graph):
     b.close()
 
 
+@pytest.mark.parametrize("precision", ["fp16", "fp16x3"])
+def test_zero_copy_out_matches_copy(precision):
+    """zero_copy_out (the default: the head writes the pixels and the post half info and the
+    newest poses into the pinned output block, no D2H copy) against the copying tick, bit for
+    bit, graph replay, over camera ticks and keypoint ticks; also with the fused pose stage
+    (pixels zero-copy, info / poses copied)."""
+    m = _model(precision)
+    for split in (True, False):
+        a, b = _pipe(m, True, split_pose=split), _pipe(m, True, split_pose=split, zero_copy_out=False)
+        for seed in range(1, 4):
+            rgb, d = _frames(seed)
+            for x, y_ in zip(a.tick(rgb, d), b.tick(rgb, d)):
+                np.testing.assert_array_equal(x, y_)
+        y = _keypoints(_truth(3, 1)[0][0])
+        for x, y_ in zip(a.tick_keypoints(y), b.tick_keypoints(y)):
+            np.testing.assert_array_equal(x, y_)
+        a.close()
+        b.close()
+
+
 def _whiten(ref):
     sp, sd, sc = SIG["proj_sigma"], SIG["dyn_sigma"], SIG["cv_sigma"]
     ref["r_proj"], ref["j_proj"] = ref["r_proj"] / sp, ref["j_proj"] / sp
@@ -259,7 +279,7 @@ def _check_tick(p, before, y_new, nvalid):
     # forward-error bound 10 cond(M) eps
     H, g, d = G.gn_step(lin, n, LW, nk, SIG["lam"])
     dd = p.gn.out["delta"].cpu().numpy().reshape(n, -1)
-    info = p.gn.out["info"].cpu().numpy()
+    info = p.info_h.numpy().copy()  # (the tick's info output: the pinned block, zero_copy_out)
     eps = np.finfo(np.float64).eps
     for t in range(n):
         M = H[t] + SIG["lam"] * np.eye(H.shape[1])

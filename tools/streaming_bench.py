@@ -24,6 +24,7 @@ def main():
     p.add_argument("--cams", type=int, default=3)
     p.add_argument("--window", type=int, default=24)
     p.add_argument("--zero-copy", type=int, default=None, help="1 / 0: the tick reads the pinned staging (no H2D copy); default per precision")
+    p.add_argument("--zero-copy-out", type=int, default=1, help="1 / 0: results written into the pinned block (no D2H copy)")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -35,7 +36,8 @@ def main():
     m = KeypointCNN(num_channels=4)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
     dev = torch.device("cuda", 0)
-    print(json.dumps(streaming_leg(m, dev, a.ticks, a.hz, a.cams, a.window, zero_copy=None if a.zero_copy is None else bool(a.zero_copy))))
+    print(json.dumps(streaming_leg(m, dev, a.ticks, a.hz, a.cams, a.window, zero_copy=None if a.zero_copy is None else bool(a.zero_copy),
+                                   zero_copy_out=bool(a.zero_copy_out))))
 
 
 if __name__ == "__main__":
