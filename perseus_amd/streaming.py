@@ -16,13 +16,17 @@ Gauss-Newton step per tick.  Per tick:
        (B = n_cams; fp16: the preprocess runs inside the stem's row loads; fp16x3 / fp32: the
        preprocess kernel, then the forward; the denormalize in the head), in the small-batch
        latency mode for fp16 and fp16x3 (the parity-grade tick)
-       [pose stage] -> pa_window_advance_n (window shifts one frame, the new keypoints
-       appended, the new pose predicted by the dynamics model, the count of real frames + 1)
-       -> pa_trajectory_linearize (whitened factors of every camera's window; frames not yet
-       filled by a real tick carry no projection factors) -> pa_trajectory_gn_step (delta and
-       info only) -> pa_window_retract_newest (pose Exp(delta), velocities += delta, newest
-       poses out) -> ONE D2H of [pixels | info | newest poses] (and one H2D of [rgb | depth]
-       at the start)
+       [pose stage] the sequence pa_window_advance_n (window shifts one frame, the new
+       keypoints appended, the new pose predicted by the dynamics model, the count of real
+       frames + 1) -> pa_trajectory_linearize (whitened factors of every camera's window;
+       frames not yet filled by a real tick carry no projection factors) ->
+       pa_trajectory_gn_step (delta and info only) -> pa_window_retract_newest (pose
+       Exp(delta), velocities += delta, newest poses out), run as the split tick for windows
+       <= 24 frames: pa_window_pose_tick_pre (all of it that does not need the new keypoints,
+       on the tick's stream while the forward runs on a second one; or, pre_ahead=True, right
+       after the previous tick's results) and pa_window_pose_tick_post after the forward
+       -> the pixels, info and newest poses land in the pinned output block (zero_copy_out;
+       else one D2H), one H2D of [rgb | depth] at the start (or zero-copy reads of it)
   host: wait for the replay, return (n_cams, K, 2) pixel coordinates (and the poses).
 
 The graph removes the per-launch CPU cost of the ~26 launches (the forward at B=3
