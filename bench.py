@@ -494,7 +494,8 @@ def per_kernel_rooflines(per_launch, B, precision):
     convs = {f"{i:02d}_{nm}": round(f / (ms * 1e-3) / MFMA_FP16_DENSE_PEAK, 4)
              for (i, nm, ms), f in zip(per_launch, fl) if nm.startswith("conv3x3")}
     return {"stem": stem, "conv3x3_mfma_frac": convs, "mfma_peak_tflops": MFMA_FP16_DENSE_PEAK / 1e12,
-            "timing": "per-launch HIP events (pa_detector_time_launch), as kernels_ms"}
+            "timing": "per-launch HIP events (pa_detector_time_launch), as kernels_ms",
+            "mfma_busy_counter": pmc_mfma(precision, B, names)}
 
 
 def factor_leg(dev, seed, rank, T=1000, L=24, reps=20):
@@ -592,14 +593,40 @@ def pmc_traffic(precision, B, idxs, names):
     return round(sum(v) / len(v))
 
 
-def px_reference(state, x_host, nframes=8):
+def pmc_mfma(precision, B, names):
+    """rocprofv3-counter MFMA utilisation of every 3x3 conv launch (tools/mfma_counters.py:
+    SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x the launch's cycles, and over the nominal
+    2.4 GHz cycles of its duration) from the committed record profiles/pmc_mfma.json, if it
+    was taken on the same kernel sources (csrc digest), launch sequence and batch; else None."""
+    tf = os.path.join(ROOT, "profiles", "pmc_mfma.json")
+    try:
+        with open(tf) as fh:
+            rec = json.load(fh).get(precision)
+    except (OSError, ValueError):
+        return None
+    if not rec or rec.get("batch") != B or rec.get("names") != names or rec.get("csrc") != csrc_digest():
+        return None
+    pl = rec["per_launch"]
+    return {"busy_frac_of_cycles": {f"{i:02d}_{r['launch']}": r["busy_frac_of_cycles"]
+                                    for i, r in enumerate(pl) if r["launch"].startswith("conv3x3")},
+            "busy_frac_of_nominal": {f"{i:02d}_{r['launch']}": r["busy_frac_of_nominal"]
+                                     for i, r in enumerate(pl) if r["launch"].startswith("conv3x3")},
+            "clock_ghz": {f"{i:02d}_{r['launch']}": r["clock_ghz"]
+                          for i, r in enumerate(pl) if r["launch"].startswith("conv3x3")},
+            "source": rec.get("source"),
+            "counters": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), and / (1024 x duration x "
+                        "2.4 GHz) (the latter comparable with conv3x3_mfma_frac)"}
+
+
+def px_reference(state, x_host, nframes=None):
     """CPU f32 reference outputs (oracle/resnet_ref.py, the reference's own CPU path
-    restated) of the first `nframes` bench frames."""
+    restated) of the bench frames: the whole benched batch by default (max /
+    mean over 64 frames x 8 keypoints; ~1 s of CPU at 16 threads), or the first `nframes`."""
     import torch
 
     from oracle import resnet_ref as R
 
-    return R.run(state, x_host[:nframes], torch.float32)
+    return R.run(state, x_host if nframes is None else x_host[:nframes], torch.float32)
 
 
 def px_error(model, x, yref):

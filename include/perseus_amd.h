@@ -57,9 +57,12 @@ int pa_detector_create(const float* weights, size_t nbytes, int in_ch, int n_kp,
                        pa_detector** out);
 void pa_detector_destroy(pa_detector* d);
 
-/* Pre-size the activation workspace for batches up to max_batch (allocation is
- * otherwise done lazily on the first larger forward; it is never done inside a
- * captured graph). */
+/* Pre-size the activation workspace for batches up to max_batch (clamped to the
+ * 1,024-frame chunk a forward runs in), and for 4-channel models in fp16x3 / fp32 also
+ * forward_rgbd's f32 input staging (a later set_precision keeps the reservation).
+ * Without it, allocation is done lazily by the first call of a larger batch, which
+ * frees the smaller buffer: capture a graph only after reserve() (or after an eager
+ * call of the same batch), and reserve the largest batch any graph will replay. */
 int pa_detector_reserve(pa_detector* d, int max_batch);
 
 /* PA_PREC_FP16 (default), PA_PREC_FP32 or PA_PREC_FP16X3. */
@@ -84,8 +87,8 @@ int pa_detector_forward(pa_detector* d, const float* x_dev, int B, float* y_dev,
  * the ZED delivers) + f32 depth in metres, both [B][Hs][Ws], centre-cropped to 256x256;
  * pa_preprocess_rgbd's arithmetic (streaming.py:68-80, deterministic near/far clip, < 0 =
  * off).  fp16: applied inside the stem's row loads, so the f32 (B,4,256,256) input is never
- * written; fp16x3 / fp32: the preprocess kernel into the handle's own f32 staging (allocated
- * by the first call of a batch size, outside any graph), then the forward.  Output
+ * written; fp16x3 / fp32: the preprocess kernel into the handle's own f32 staging (sized by
+ * pa_detector_reserve, else by the first call of a larger batch), then the forward.  Output
  * bit-identical to pa_preprocess_rgbd + pa_detector_forward.  4-channel models only. */
 int pa_detector_forward_rgbd(pa_detector* d, const uint8_t* rgb_dev, const float* depth_dev, int B, int Hs, int Ws,
                              int bgr, float near_m, float far_m, float* y_dev, void* stream);

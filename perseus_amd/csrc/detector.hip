@@ -64,6 +64,7 @@ struct pa_detector {
   float* part = nullptr;                       // its f32 partials (splitk_part_floats(splitk_max))
   float* xin = nullptr;                        // forward_rgbd's f32 input staging (fp16x3 / fp32)
   int xin_cap = 0;
+  int reserved = 0;                            // largest pa_detector_reserve batch (clamped to a chunk)
 };
 
 namespace pa {
@@ -762,7 +763,14 @@ void pa_detector_destroy(pa_detector* d) {
 int pa_detector_reserve(pa_detector* d, int max_batch) {
   PA_CHECK(d && max_batch >= 0, "bad arguments");
   // forward / forward_rgbd never use more than one chunk's workspace
-  return pa::ensure_ws(d, max_batch < pa::kChunk ? max_batch : pa::kChunk);
+  const int n = max_batch < pa::kChunk ? max_batch : pa::kChunk;
+  PA_TRY(pa::ensure_ws(d, n));
+  // forward_rgbd's f32 staging (fp16x3 / fp32 on a 4-channel model): reserved here too, so
+  // that a graph captured after reserve() never allocates, and never keeps a pointer that a
+  // later larger call frees
+  if (d->in_ch == 4 && d->prec != PA_PREC_FP16) PA_TRY(pa::ensure_xin(d, n));
+  d->reserved = n > d->reserved ? n : d->reserved;
+  return PA_OK;
 }
 
 int pa_detector_set_split_k(pa_detector* d, int max_batch) {
@@ -793,7 +801,9 @@ int pa_detector_set_precision(pa_detector* d, int precision) {
     int bcap = 0;
     while (bcap < pa::kChunk && pa::ws_need(bcap + 1, d->prec) <= old) ++bcap;
     d->prec = precision;
-    if (bcap > 0) return pa::ensure_ws(d, bcap);
+    if (bcap > 0) PA_TRY(pa::ensure_ws(d, bcap));
+    // a reservation covers forward_rgbd's staging in the new precision too
+    if (d->reserved > 0 && d->in_ch == 4 && precision != PA_PREC_FP16) PA_TRY(pa::ensure_xin(d, d->reserved));
   }
   return PA_OK;
 }

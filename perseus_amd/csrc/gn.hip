@@ -1647,14 +1647,16 @@ __global__ __launch_bounds__(64 * GN_CR_W, 1) void pose_tick_post_kernel(pa_traj
 // assembler waves per trajectory and solver (pa_debug_gn_set_assemblers: na + 8 * legacy;
 // 0 = the shipped choice)
 static int g_gn_na = 0;
+// CUs of the CURRENT device (cached per device id: a host with GPUs of different CU counts
+// gets each one's own); only the cyclic-reduction vs two-ended choice in launch_gn uses it
 static int g_gn_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
+  static int cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  if (dev < 64 && cache[dev] > 0) return cache[dev];
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  if (dev < 64) cache[dev] = n;
   return n;
 }
 static unsigned long long* g_gn_trace = nullptr;
@@ -1713,9 +1715,10 @@ int pa_window_pose_tick(const pa_traj_args* ta, const float* y_new, double lambd
                         double* newest_pose, void* stream) {
   PA_CHECK(ta && y_new && delta && info, "pose tick: null args / y_new / delta / info");
   const int T = ta->T, L = ta->L, K = ta->n_kp;
-  PA_CHECK(T >= 0 && T <= pa::g_gn_cus() && L >= 2 && L <= pa::GN_CR_LMAX && K >= 0 && K <= pa::GN_KMAX,
-           "pose tick: T %d (<= %d CUs), L %d (2..%d), n_kp %d (<= %d)", T, pa::g_gn_cus(), L, pa::GN_CR_LMAX, K,
-           pa::GN_KMAX);
+  // one workgroup per trajectory: correct at any T (the CU count is a performance choice of the
+  // caller, StreamingPipeline's fused_pose / split_pose eligibility)
+  PA_CHECK(T >= 0 && L >= 2 && L <= pa::GN_CR_LMAX && K >= 0 && K <= pa::GN_KMAX,
+           "pose tick: T %d, L %d (2..%d), n_kp %d (<= %d)", T, L, pa::GN_CR_LMAX, K, pa::GN_KMAX);
   if (T == 0) return PA_OK;
   PA_CHECK(lambda >= 0.0, "pose tick: lambda %g < 0", lambda);
   PA_CHECK(ta->y && ta->pose && ta->vel && ta->angvel && ta->corners && ta->K && ta->nvalid,
@@ -1750,9 +1753,8 @@ size_t pa_window_pose_tick_workspace(int T, int L) {
 static int pose_tick_check(const pa_traj_args* ta, const char* who) {
   PA_CHECK(ta, "%s: null args", who);
   const int T = ta->T, L = ta->L, K = ta->n_kp;
-  PA_CHECK(T >= 0 && T <= pa::g_gn_cus() && L >= 2 && L <= pa::GN_CR_LMAX && K >= 0 && K <= pa::GN_KMAX,
-           "%s: T %d (<= %d CUs), L %d (2..%d), n_kp %d (<= %d)", who, T, pa::g_gn_cus(), L, pa::GN_CR_LMAX, K,
-           pa::GN_KMAX);
+  PA_CHECK(T >= 0 && L >= 2 && L <= pa::GN_CR_LMAX && K >= 0 && K <= pa::GN_KMAX,
+           "%s: T %d, L %d (2..%d), n_kp %d (<= %d)", who, T, L, pa::GN_CR_LMAX, K, pa::GN_KMAX);
   PA_CHECK(ta->y && ta->pose && ta->vel && ta->angvel && ta->corners && ta->K && ta->nvalid,
            "%s: null window / model pointer", who);
   PA_CHECK((K == 0 || (ta->r_proj && ta->j_proj && ta->status)) && ta->r_dyn && ta->j_dyn0 && ta->j_dyn1 &&

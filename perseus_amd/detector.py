@@ -206,9 +206,14 @@ class KeypointCNN(nn.Module):
         return super().train(False)
 
     def reserve(self, max_batch: int, device=None):
+        """pa_detector_reserve in this model's precision: the workspace (and for fp16x3 / fp32
+        the RGBD staging of forward_rgbd) for batches up to `max_batch`, so that a graph
+        captured afterwards allocates nothing."""
         device = torch.device(device or torch.device("cuda", torch.cuda.current_device()))
         h = self._ensure_handle(device)
-        _lib.check(_lib.lib().pa_detector_reserve(h, max_batch), "reserve")
+        L = _lib.lib()
+        _lib.check(L.pa_detector_set_precision(h, _lib.precision_code(self.precision)), "set_precision")
+        _lib.check(L.pa_detector_reserve(h, max_batch), "reserve")
 
     def flops_per_frame(self) -> float:
         dev = torch.device("cuda", torch.cuda.current_device())

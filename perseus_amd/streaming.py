@@ -38,6 +38,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import warnings
+
 import numpy as np
 import torch
 
@@ -279,6 +281,16 @@ class StreamingPipeline:
         # (in the gap before the next camera frames), so a tick's latency path is H2D, forward,
         # post half, D2H.  The window and factor outputs then already hold the next tick's advance.
         self.pre_ahead = self.split_pose and self._pre_ahead_req
+        if self._pre_ahead_req and not self.pre_ahead:  # never drop the request silently
+            why = ("split_pose=False" if not self._split_pose_req else
+                   f"pose_window {Lw} > {pipeline.TICK_MAX_L}" if Lw > pipeline.TICK_MAX_L else
+                   f"{n} cameras > the device's CUs")
+            warnings.warn(f"StreamingPipeline: pre_ahead needs the split pose tick ({why}); running the full-latency "
+                          f"tick (self.pre_ahead is False)", RuntimeWarning, stacklevel=3)
+        if self.split_pose and self._zc_out:
+            # the post half writes info and the newest poses straight into the pinned output block
+            # (self.info_h / self.pose_h); nothing writes a device copy, so none is exposed
+            self.gn.out["info"] = None
         self.tick_ws = pipeline.window_pose_tick_workspace(n, Lw, dev)
         self.side = torch.cuda.Stream(dev)
 
@@ -347,7 +359,13 @@ class StreamingPipeline:
 
     def tick(self, rgb: np.ndarray, depth: np.ndarray):
         """One camera tick through the pose stage: (pixels (n, K, 2), newest pose of each
-        camera's window (n, 12: R row-major, t), GN info (n,) int32, 0 = solved)."""
+        camera's window (n, 12: R row-major, t), GN info (n,) int32, 0 = solved).
+
+        The results are read from the pinned output block (self.px_h / pose_h / info_h), the
+        only place every tick form writes them.  With pre_ahead, the next tick's pre half has
+        already run when this returns: self.win, self.lin (the factor outputs, status 3 on
+        the newest frame's projection factors) and the tick workspace hold the NEXT tick's
+        advanced window, not this tick's (window_state() says the same)."""
         if not self.pose_L:
             raise RuntimeError("tick() needs the pose stage (pose_window > 0)")
         px = self(rgb, depth)
@@ -357,7 +375,9 @@ class StreamingPipeline:
         """The pose stage alone on given normalized keypoints y (n, 2K) (the detector's output
         convention, validate.py:139-141): the same launches as a tick's pose stage, from
         self.y, captured as their own graph when graph=True.  Returns (newest pose (n, 12),
-        GN info (n,)).  For driving the smoother with known measurements."""
+        GN info (n,)).  For driving the smoother with known measurements.  As tick(): the
+        results come from the pinned output block, and under pre_ahead self.win / self.lin
+        already hold the next tick's pre half."""
         if not self.pose_L:
             raise RuntimeError("tick_keypoints() needs the pose stage (pose_window > 0)")
         self.y_h.numpy()[:] = np.asarray(y, np.float32).reshape(self.y_h.shape)

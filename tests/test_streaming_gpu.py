@@ -158,3 +158,28 @@ def test_zero_copy_tick_matches_copying_tick(model, model_x3, precision):
             np.testing.assert_array_equal(x, z)
     for p in (a, b, c):
         p.close()
+
+
+@pytest.mark.parametrize("precision", ["fp16x3", "fp32"])
+def test_reserve_then_capture_forward_rgbd(precision):
+    """reserve() sizes forward_rgbd's f32 staging too, so a graph captured with NO
+    eager call before it allocates nothing and replays to the eager bits; a later larger
+    eager call may regrow the buffers, so the graph is replayed before it."""
+    m = KeypointCNN(num_channels=4, precision=precision)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
+    dev = torch.device("cuda", 0)
+    rgb, d = _frames(21, n=3, Hs=300, Ws=400)
+    rgb_d, d_d = torch.as_tensor(rgb).to(dev), torch.as_tensor(d).to(dev)
+    m.reserve(3, dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        y_graph = m.forward_rgbd(rgb_d, d_d)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    got = y_graph.clone()
+    want = m.forward_rgbd(rgb_d, d_d)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(got, want)
+    assert torch.isfinite(got).all()

@@ -391,3 +391,21 @@ def test_fused_pose_tick_limits(model):
         _, info = p.tick_keypoints(_keypoints(truth[k]))
     assert (info == 0).all()
     p.close()
+
+
+def test_pre_ahead_request_is_never_dropped_silently(model):
+    """pre_ahead needs the split tick; without it the pipeline warns and reports
+    pre_ahead False.  With split + zero-copy output, the GN info lives only in the pinned
+    block: no stale device buffer is exposed as gn.out['info']."""
+    with pytest.warns(RuntimeWarning, match="pre_ahead"):
+        p = StreamingPipeline(model, graph=False, pose_window=4, split_pose=False, pre_ahead=True, **SIG)
+    assert not p.pre_ahead and not p.split_pose
+    p.close()
+    p0, v0, w0 = _init()
+    q = StreamingPipeline(model, graph=False, pose_window=4, zero_copy_out=True, init_pose=p0, init_vel=v0,
+                          init_angvel=w0, **SIG)
+    assert q.split_pose and q.gn.out["info"] is None
+    truth, _, _ = _truth(3, 3)
+    _, info = q.tick_keypoints(_keypoints(truth[0]))
+    assert (info == 0).all()
+    q.close()

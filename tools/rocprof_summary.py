@@ -1,4 +1,4 @@
-"""Summarise a tools/profile_round.sh output directory into profiles/.
+"""Summarise a `tools/gpu_check.sh profile` output directory into profiles/.
 
     python tools/rocprof_summary.py --dir gpurun_out/r01 --tag r01
 
