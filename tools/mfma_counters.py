@@ -9,16 +9,19 @@ blocks"), for the kernels of the current csrc digest.
 
 Normalisation (MI355X_MICROARCH.md, "Per-instruction cycle constants" and "DVFS give-back"):
 SQ_VALU_MFMA_BUSY_CYCLES is summed over every SIMD of the chip and counts shader cycles (16 per
-v_mfma_f32_16x16x32_f16, 32 per 32x32x16); GRBM_GUI_ACTIVE is summed over the 8 XCDs, so one
-XCD's count, GRBM_GUI_ACTIVE / 8, is the launch's length in shader cycles.  Hence
+v_mfma_f32_16x16x32_f16, 32 per 32x32x16); SQ_BUSY_CYCLES is summed over the 32 shader engines,
+so SQ_BUSY_CYCLES / 32 is the launch's busy span in shader cycles (it agrees with SQ_WAVE_CYCLES
+per wave x 4, the waves living the whole launch).  Hence
 
-    busy fraction of the launch's cycles = MFMA_BUSY / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
     fraction of the nominal peak          = MFMA_BUSY / (1024 SIMDs x duration x 2.4 GHz)
+    busy fraction of the launch's cycles = MFMA_BUSY / (1024 SIMDs x SQ_BUSY_CYCLES / 32)
+    clock the chip held                   = SQ_BUSY_CYCLES / 32 / duration
 
-(the second is the same quantity as bench.py's FLOPs / (time x 2.5 PF) when the MFMAs are
-16x16x32 f16: 16 cycles x 1024 FLOP/cycle/SIMD = 16,384 FLOP each), and the clock the chip held is
-GRBM_GUI_ACTIVE / 8 / duration.  The old tools/pmc_table.py column divided by GRBM_GUI_ACTIVE
-itself (8 XCDs' worth of cycles) and read ~8x low.
+(the first is the same quantity as bench.py's FLOPs / (time x 2.5 PF) when the MFMAs are
+16x16x32 f16: 16 cycles x 1024 FLOP/cycle/SIMD = 16,384 FLOP each; the second removes the DVFS
+give-back).  GRBM_GUI_ACTIVE / 8 / duration reads 2.6-3.2 GHz on these ~20 us dispatches (the
+guide: it reads high below ~0.3 ms), so it is recorded but not used.  The old
+tools/pmc_table.py column divided by GRBM_GUI_ACTIVE itself (8 XCDs' worth) and read ~8x low.
 
 Writes profiles/<tag>_mfma_counters.txt and the digest-keyed record profiles/pmc_mfma.json
 (bench.py reports it as per_kernel_roofline.mfma_busy_counter when the digest matches).
@@ -84,19 +87,20 @@ def main():
     if not hits:
         raise SystemExit(f"no counter csv under {a.dir}/mfma")
     syms, per = summarise(dispatches(hits[0]), len(names))
-    fl = conv_flops(B) if prec == "fp16" and len(conv_flops(B)) == len(names) else [None] * len(names)
+    cf = conv_flops(B, fused_head=names[-1] != "avgpool_fc")
+    fl = cf if prec == "fp16" and len(cf) == len(names) else [None] * len(names)
     lines = [f"# MFMA counters {a.tag} ({prec}, batch {B}; csrc {meta.get('csrc')})", "",
              "rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE over "
-             "tools/pmc_forward.py (plain forwards), median per launch over forwards; busy/cycles = "
-             "MFMA_BUSY / (1024 SIMDs x GUI_ACTIVE/8); busy/nominal = MFMA_BUSY / (1024 x dur x 2.4 GHz); "
-             "clock = GUI_ACTIVE/8/dur; FLOP ratio = MFMA FLOPs executed / algorithmic FLOPs (padding).", "",
+             "tools/pmc_forward.py (plain forwards), median per launch over forwards; busy/nominal = "
+             "MFMA_BUSY / (1024 SIMDs x dur x 2.4 GHz) (= bench.py's conv3x3_mfma_frac quantity); busy/cycles = "
+             "MFMA_BUSY / (1024 x SQ_BUSY_CYCLES/32); clock = SQ_BUSY_CYCLES/32/dur; FLOP ratio = MFMA FLOPs executed / algorithmic FLOPs (padding).", "",
              "| # | launch | dur us | MFMA insts | MFMA busy cyc | cyc/MFMA | clock GHz | busy/cycles | busy/nominal "
              "| FLOP ratio |", "|---|---|---|---|---|---|---|---|---|---|"]
     rec = []
     for i, (nm, c) in enumerate(zip(names, per)):
-        gui8 = c["GRBM_GUI_ACTIVE"] / 8
-        ghz = gui8 / (c["dur_us"] * 1e3) if c["dur_us"] > 0 else 0.0
-        fc = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * gui8) if gui8 else 0.0
+        cyc = c["SQ_BUSY_CYCLES"] / 32  # 32 shader engines
+        ghz = cyc / (c["dur_us"] * 1e3) if c["dur_us"] > 0 else 0.0
+        fc = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cyc) if cyc else 0.0
         fn = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * c["dur_us"] * 1e3 * NOMINAL_GHZ) if c["dur_us"] else 0.0
         cpm = c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["SQ_INSTS_MFMA"] if c["SQ_INSTS_MFMA"] else 0.0
         ratio = (c["SQ_INSTS_MFMA"] * FLOP_PER_MFMA / fl[i]) if fl[i] else None

@@ -51,9 +51,10 @@ def main():
         gui = c.get("GRBM_GUI_ACTIVE", 1)
         mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
         waves = c.get("SQ_WAVES", 0)
-        # MFMA busy cycles are summed over the 1024 SIMDs; GRBM_GUI_ACTIVE over the 8 XCDs, so
-        # GUI_ACTIVE / 8 is the launch's length in cycles (tools/mfma_counters.py)
-        print(f"{i:2d} {names[i]:20s} {mf / max(1024 * gui / 8, 1):8.3f} {100 * c['SQ_WAIT_ANY'] / wc:8.1f} "
+        # MFMA busy cycles are summed over the 1024 SIMDs, SQ_BUSY_CYCLES over the 32 shader engines
+        # (tools/mfma_counters.py; GRBM_GUI_ACTIVE reads high on dispatches this short)
+        sqb = c.get("SQ_BUSY_CYCLES", 8 * gui) / 32
+        print(f"{i:2d} {names[i]:20s} {mf / max(1024 * sqb, 1):8.3f} {100 * c['SQ_WAIT_ANY'] / wc:8.1f} "
               f"{100 * c['SQ_WAIT_INST_ANY'] / wc:9.1f} {100 * c['SQ_ACTIVE_INST_ANY'] / wc:7.1f} "
               f"{100 * c.get('SQ_WAIT_INST_LDS', 0) / wc:8.1f} "
               f"{c.get('SQ_LDS_BANK_CONFLICT', 0) / max(c.get('SQ_LDS_IDX_ACTIVE', 1), 1):7.3f} "
