@@ -30,6 +30,8 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mllvm", "-disable-promote-alloca-to-lds
 
 
 OBJDIR = os.path.join(LIBDIR, "obj")  # incremental build state (git- and gpurun-ignored)
+# per-source extra hipcc flags (file name -> list); part of the flags digest
+EXTRA: dict = {}
 
 
 CXX = os.environ.get("CXX_HOST", "g++")
@@ -62,6 +64,9 @@ def _includes(path, seen=None):
 
 
 STAMP = os.path.join(OBJDIR, "flags.stamp")
+# the same digest beside the library (git-ignored, travels with it to the GPU box, where obj/ does
+# not): a fresh tree with an up-to-date .so needs no rebuild
+LIB_STAMP = LIB + ".flags"
 
 
 def _flags_digest() -> str:
@@ -69,7 +74,7 @@ def _flags_digest() -> str:
     object (mtimes alone would link stale objects built with the old flags)."""
     import hashlib
 
-    return hashlib.sha256(repr((HIPCC, FLAGS, ARCH, CXX, HOST_FLAGS)).encode()).hexdigest()
+    return hashlib.sha256(repr((HIPCC, FLAGS, ARCH, CXX, HOST_FLAGS, sorted(EXTRA.items()))).encode()).hexdigest()
 
 
 def _stamp_ok() -> bool:
@@ -92,8 +97,16 @@ def _stale(src: str) -> bool:
     return any(os.path.getmtime(p) > t for p in [src, *_includes(src)])
 
 
+def _lib_stamp_ok() -> bool:
+    try:
+        with open(LIB_STAMP) as fh:
+            return fh.read().strip() == _flags_digest()
+    except OSError:
+        return False
+
+
 def up_to_date() -> bool:
-    if not os.path.exists(LIB) or not _stamp_ok():
+    if not os.path.exists(LIB) or not (_stamp_ok() or _lib_stamp_ok()):
         return False
     t = os.path.getmtime(LIB)
     return all(os.path.getmtime(p) <= t for p in _deps())
@@ -104,7 +117,7 @@ def _compile(src: str) -> str:
     if src.endswith(".cpp"):
         cmd = [CXX, *HOST_FLAGS, "-c", src, "-o", obj + ".tmp"]
     else:
-        cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj + ".tmp"]
+        cmd = [HIPCC, *FLAGS, *EXTRA.get(os.path.basename(src), []), "-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"{cmd[0]} failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -134,8 +147,9 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB)
-    with open(STAMP, "w") as fh:
-        fh.write(_flags_digest() + "\n")
+    for st in (STAMP, LIB_STAMP):
+        with open(st, "w") as fh:
+            fh.write(_flags_digest() + "\n")
     if verbose:
         print(f"built {LIB} ({len(todo)} of {len(srcs)} objects recompiled)")
     return LIB
