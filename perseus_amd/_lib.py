@@ -125,8 +125,10 @@ def lib(build_if_missing: bool = True):
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = _build.LIB
-    if not os.path.exists(path) and build_if_missing:
+    # PERSEUS_AMD_LIB_AB: another build of the library, for tools/so_ab.py's interleaved A/B of
+    # two builds on one box (measurement tooling only; unset, the in-tree build is the library)
+    path = os.environ.get("PERSEUS_AMD_LIB_AB") or _build.LIB
+    if not os.path.exists(path) and build_if_missing and path == _build.LIB:
         _build.build()
     if not os.path.exists(path):
         raise PerseusError(f"{path} not found: run `python -m perseus_amd.build`")

@@ -29,7 +29,8 @@ static_assert(PJ == 5 * NWAVE + 1, "patch DMA split: 5 per wave + 1 on wave 0");
 static_assert(WBYTES + 2 * PATCHB <= 160 * 1024, "LDS");
 }  // namespace c64d
 
-// DBG: 4 = s_memrealtime stamps into a.trace (as conv_c64.hip)
+// DBG: 4 = s_memrealtime stamps into a.trace (as conv_c64.hip); timing only (wrong results):
+// 5 = the epilogue computed but not stored, 6 = no hand-over barrier between tiles
 template <int EPI, int DBG = 0, bool WT = false>
 __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
   using namespace c64d;
@@ -39,7 +40,7 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
   char* wl = smem;
   char* patch = smem + WBYTES;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, r16 = lane & 15;
   const int H = a.Hout, W = a.Wout;
   const _Float16* __restrict__ in = (const _Float16*)a.in;
@@ -58,13 +59,26 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
     pcol[i] = p - (p / PW) * PW;
     pch[i] = ((c & 7) ^ ((p >> 1) & 7)) * 8;
   }
-  auto dma_patch = [&](int i, int tile, int buf) __attribute__((always_inline)) {
-    const int img = tile / tpi, rem = tile - img * tpi;
-    const int h = (rem / tw_n) * TH + prow[i] - 1, x = (rem - (rem / tw_n) * tw_n) * TW + pcol[i] - 1;
-    const void* src = ((unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W)
-                          ? (const void*)(in + (((size_t)img * H + h) * W + x) * 64 + pch[i])
-                          : (const void*)gx_zero_line;
-    xdma16(src, patch + buf * PATCHB + (i < 5 ? i * NWAVE + wid : 5 * NWAVE) * 1024);
+  // patch DMAs through a buffer resource over the whole input: the halo (and every DMA of a tile
+  // that does not exist) reads zeros through an out-of-range offset, so a DMA in the K loop is one
+  // offset computation and no branch.  (The pointer form -- the tile decomposed by integer
+  // division at every call, a divergent branch around the halo select, the zero line's address
+  // loaded through the GOT behind an s_waitcnt lgkmcnt(0) that also drained the fragment reads --
+  // cost the K loop of every tile ~1.3 us on the younger waves, r05h trace.)
+  const s2w_u4 rsrc = s2w_rsrc(in, (unsigned)((size_t)a.B * H * W * 128 < 0x7fffffffu ? (size_t)a.B * H * W * 128 : 0x7fffffffu));
+  struct Org {
+    int img, h0, x0;  // patch origin of a tile: image, first input row and column (halo included)
+    bool on;          // false: no such tile (every lane reads zeros)
+  };
+  auto origin = [&](int t, bool on) __attribute__((always_inline)) {
+    const int img = t / tpi, rem = t - img * tpi;
+    return Org{img, (rem / tw_n) * TH - 1, (rem - (rem / tw_n) * tw_n) * TW - 1, on};
+  };
+  auto dma_patch = [&](int i, const Org& o, int buf) __attribute__((always_inline)) {
+    const int h = o.h0 + prow[i], x = o.x0 + pcol[i];
+    const bool ok = o.on && (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W;
+    const unsigned vo = ok ? (unsigned)((((o.img * H + h) * W + x) * 64 + pch[i]) * 2) : S2W_OOB;
+    s2w_dma16(rsrc, vo, patch + buf * PATCHB + (i < 5 ? i * NWAVE + wid : 5 * NWAVE) * 1024);
   };
 
   const int o = xfrag(r16);
@@ -84,9 +98,12 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
   // prologue: patch of the first tile, then the 9 weight taps (tap i = DMA i of
   // every wave); the first tile waits for each tap just before it reads it
   int tile = blockIdx.x;
-  if (wid == 0) dma_patch(5, tile, 0);
+  {
+    const Org o0 = origin(tile, true);
+    if (wid == 0) dma_patch(5, o0, 0);
 #pragma unroll
-  for (int i = 0; i < 5; ++i) dma_patch(i, tile, 0);
+    for (int i = 0; i < 5; ++i) dma_patch(i, o0, 0);
+  }
   {
     const int row0 = wid * 8 + (lane >> 3);  // row within the tap
     const int lc = (lane & 7) ^ ((row0 >> 1) & 7);
@@ -102,6 +119,7 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
     const int buf = t & 1;
     const int next = tile + gridDim.x;
     const bool has_next = next < ntiles;
+    const Org onext = origin(has_next ? next : tile, has_next);  // (no next tile: zeros into the idle buffer)
     const int img = tile / tpi, rem = tile - img * tpi;
     const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
     size_t pixo[TM];
@@ -157,10 +175,7 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
         constexpr int R = (EPI & EPI_RES) ? TM * TN / 2 : 0;
         constexpr int J = (K - 1) / 2 < 5 ? (K - 1) / 2 : 5;
         if (t == 0) {
-          if (has_next)
-            xwait_vm<8 - TAPN + R + J>();
-          else
-            xwait_vm<8 - TAPN + R>();
+          xwait_vm<8 - TAPN + R + J>();
           lds_barrier();
         }
       }
@@ -168,12 +183,10 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
       // next tile's patch: wave 0's extra DMA at group 0, then one per odd group
       if constexpr (K == 0 || (K % 2 == 1 && K / 2 < 5)) {
         __builtin_amdgcn_sched_barrier(0);
-        if (has_next) {
-          if constexpr (K == 0) {
-            if (wid == 0) dma_patch(5, next, buf ^ 1);
-          } else {
-            dma_patch(K / 2, next, buf ^ 1);
-          }
+        if constexpr (K == 0) {
+          if (wid == 0) dma_patch(5, onext, buf ^ 1);
+        } else {
+          dma_patch(K / 2, onext, buf ^ 1);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -197,12 +210,12 @@ __global__ __launch_bounds__(512) void conv3x3_c64d(ConvArgs a, int ntiles) {
           if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
           hv[j] = (_Float16)fmaxf(v, 0.f);
         }
-        store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), hv);
+        if (DBG != 5 || a.epi < 0) store16<WT>(out, (unsigned)((pixo[tm] + p * 32) * 2), hv);
       }
     if constexpr (DBG == 4) trace_stamp(a.trace, 3 + 4 * t);
     // every wave's DMAs into buf ^ 1 landed (its wait above) and its reads of buf
     // retired (the MFMAs consumed them): one barrier hands both buffers over
-    lds_barrier();
+    if constexpr (DBG != 6) lds_barrier();
     if constexpr (DBG == 4) trace_stamp(a.trace, 5 + 4 * t);
   }
   if constexpr (DBG == 4) {
@@ -255,6 +268,8 @@ int launch_conv3x3_c64d(const ConvArgs& a, int variant, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "c64d conv: epilogue %d", a.epi);
   if (a.B <= 0) return PA_OK;
   if (variant == 4 && a.trace) return run_c64d<4>(a, s);
+  if (variant == 5) return run_c64d<5, true>(a, s);
+  if (variant == 6) return run_c64d<6, true>(a, s);
   return variant == 2 ? run_c64d<0, false>(a, s) : run_c64d<0, true>(a, s);  // 2: plain (write-back) stores
 }
 

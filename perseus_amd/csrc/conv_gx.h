@@ -88,6 +88,31 @@ __device__ __forceinline__ void xdma16(const void* src, char* lds) {
 #endif
 }
 
+// 16 B per lane from a buffer resource -> LDS (wave-uniform LDS base + lane * 16), as inline
+// asm like xdma16 (its waits are explicit).  A lane whose 32-bit byte offset is
+// out of the resource's range (S2W_OOB) reads zeros: the halo needs no pointer select and
+// the per-lane address is one 32-bit VGPR (the 64-bit pointer math of xdma16 kept ~75
+// VGPRs live across this kernel's unrolled loop and spilled).
+typedef unsigned s2w_u4 __attribute__((ext_vector_type(4)));
+constexpr unsigned S2W_OOB = 0x80000000u;
+__device__ __forceinline__ s2w_u4 s2w_rsrc(const void* base, unsigned bytes) {
+  // wave-uniform by construction; readfirstlane puts it in SGPRs for the asm's "s" operand
+  const unsigned long long b = (unsigned long long)base;
+  return s2w_u4{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)b),
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32) & 0xffffu),
+                (unsigned)__builtin_amdgcn_readfirstlane(bytes), 0x00020000u};
+}
+__device__ __forceinline__ void s2w_dma16(s2w_u4 rsrc, unsigned voff, char* lds) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const unsigned off = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) char*)lds);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in these kernels keeps it live
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(off), "v"(voff),
+               "s"(rsrc) : "memory", "m0");
+#pragma clang diagnostic pop
+#endif
+}
+
 // Issue schedule (per wave), used at compile time.
 struct GxPlan {
   int nsteps, ncb, pd, wdma, pdma, rl, rs, g;
@@ -326,7 +351,6 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int CF = PART ? PART * CIN : CIN;
   constexpr int kin = XS * CF;
   const int kc0 = PART ? CIN * (int)blockIdx.y : 0;
-  const _Float16* __restrict__ in = (const _Float16*)a.in + kc0;
   const _Float16* __restrict__ w = (const _Float16*)a.w + kc0;
 
   const int Cout = a.Cout;
@@ -356,7 +380,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
   const int n0 = tn_idx * BN;
 
-  const char* psrc[PDMA];
+  // patch DMAs through a buffer resource over this tile's images: one 32-bit byte offset per lane
+  // and DMA, computed once; a block adds a constant; halo / padding lanes hold an out-of-range
+  // offset (S2W_OOB + a block offset stays out of range) and read zeros (no pointer select)
+  const s2w_u4 prs = s2w_rsrc((const _Float16*)a.in + (size_t)img0 * H * W * kin,
+                              (unsigned)((size_t)(a.B - img0 < NI ? a.B - img0 : NI) * H * W * kin * 2));
+  unsigned poff[PDMA];
 #pragma unroll
   for (int i = 0; i < PDMA; ++i) {
     const int c = (i * NW + wid) * 64 + lane;
@@ -366,14 +395,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     const int pr = pp / PW, pcl = pp - (pp / PW) * PW;
     const int n = img0 + img, h = th0 + pr - 1, x = tw0 + pcl - 1;
     const bool ok = p < NP && pr < PH && n < a.B && (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W;
-    psrc[i] = ok ? (const char*)(in + (((size_t)n * H + h) * W + x) * kin + lc * 8) : nullptr;
+    poff[i] = ok ? (unsigned)((((img * H + h) * W + x) * kin + kc0 + lc * 8) * 2) : S2W_OOB;
   }
   auto dma_patch = [&](int vb, int buf) __attribute__((always_inline)) {
+    const unsigned bo = (unsigned)(gx_boff<NCB, CF>(VB::pblk(vb)) * 2);
 #pragma unroll
-    for (int i = 0; i < PDMA; ++i) {
-      const char* s = psrc[i] ? psrc[i] + gx_boff<NCB, CF>(VB::pblk(vb)) * 2 : (const char*)gx_zero_line;
-      xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
-    }
+    for (int i = 0; i < PDMA; ++i) s2w_dma16(prs, poff[i] + bo, patch + buf * PATCHB + (i * NW + wid) * 1024);
   };
   const _Float16* wsrc[WDMA];
 #pragma unroll

@@ -83,31 +83,6 @@ struct S2wPlan {
 __host__ __device__ constexpr int s2w_tap(int t) { return t < 3 ? 3 + t : (t == 3 ? -1 : (t < 7 ? t - 4 : t - 1)); }
 __host__ __device__ constexpr int s2w_kw(int t) { return t < 3 ? t : (t == 3 ? 1 : (t < 7 ? t - 4 : t - 7)); }
 
-// 16 B per lane from a buffer resource -> LDS (wave-uniform LDS base + lane * 16), as inline
-// asm like conv_gx.h's xdma16 (its waits are explicit).  A lane whose 32-bit byte offset is
-// out of the resource's range (S2W_OOB) reads zeros: the halo needs no pointer select and
-// the per-lane address is one 32-bit VGPR (the 64-bit pointer math of xdma16 kept ~75
-// VGPRs live across this kernel's unrolled loop and spilled).
-typedef unsigned s2w_u4 __attribute__((ext_vector_type(4)));
-constexpr unsigned S2W_OOB = 0x80000000u;
-__device__ __forceinline__ s2w_u4 s2w_rsrc(const void* base, unsigned bytes) {
-  // wave-uniform by construction; readfirstlane puts it in SGPRs for the asm's "s" operand
-  const unsigned long long b = (unsigned long long)base;
-  return s2w_u4{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)b),
-                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32) & 0xffffu),
-                (unsigned)__builtin_amdgcn_readfirstlane(bytes), 0x00020000u};
-}
-__device__ __forceinline__ void s2w_dma16(s2w_u4 rsrc, unsigned voff, char* lds) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const unsigned off = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) char*)lds);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in these kernels keeps it live
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(off), "v"(voff),
-               "s"(rsrc) : "memory", "m0");
-#pragma clang diagnostic pop
-#endif
-}
-
 // X3 (fp16x3 parity mode, conv_gx.h X3): activation planes [hi (CIN) | lo (CIN)] per pixel,
 // weights hi / lo planes of w * 2^e; a unit is one of the 3 virtual blocks per 64 channels
 // (GxBlocks), the epilogue unscales exactly and writes (hi, lo) plane pairs.

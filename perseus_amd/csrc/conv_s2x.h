@@ -117,9 +117,16 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
   };
 
   // patch DMA: LDS slot c = (i * NW + wid) * 64 + lane holds position p = c >> 3,
-  // logical chunk (c & 7) ^ swizzle(p); block blk = tile j's virtual block vb
-  auto dma_patch = [&](int blk, int buf) __attribute__((always_inline)) {
-    const int j = blk / VB::NVB, vb = blk - (blk / VB::NVB) * VB::NVB;
+  // logical chunk (c & 7) ^ swizzle(p); block blk = tile j's virtual block vb.  Through a
+  // buffer resource over this image (conv_gx.h s2w_dma16): the per-lane byte offset of a tile
+  // is computed once (tile_off), a block adds a constant, and halo / padding lanes carry an
+  // out-of-range offset (S2W_OOB + block offset stays out of range) and read zeros.  (The
+  // pointer form recomputed the tile, selected a 64-bit pointer against a zero line whose
+  // address came through the GOT behind s_waitcnt lgkmcnt(0) -- draining the fragment reads --
+  // at every DMA of the K loop.)
+  const s2w_u4 prs = s2w_rsrc((const _Float16*)a.in + (size_t)img * Hin * Win * kin,
+                              (unsigned)((size_t)Hin * Win * kin * 2));
+  auto tile_off = [&](int j, unsigned (&po)[PDMA]) __attribute__((always_inline)) {
     int th0, tw0;
     tile_origin(j, th0, tw0);
 #pragma unroll
@@ -131,11 +138,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
       const int col = pos <= TW ? 2 * pos : 2 * (pos - TW - 1) + 1;
       const int h = 2 * th0 - 1 + pr, x = 2 * tw0 - 1 + col;
       const bool ok = p < NP && pos < 2 * TW + 1 && (unsigned)h < (unsigned)Hin && (unsigned)x < (unsigned)Win;
-      const char* s = ok ? (const char*)(in + (((size_t)img * Hin + h) * Win + x) * kin + lc * 8 +
-                                         gx_boff<NCB, CF>(VB::pblk(vb)))
-                         : (const char*)gx_zero_line;
-      xdma16(s, patch + buf * PATCHB + (i * NW + wid) * 1024);
+      po[i] = ok ? (unsigned)(((h * Win + x) * kin + kc0 + lc * 8) * 2) : S2W_OOB;
     }
+  };
+  unsigned poff[PDMA];
+  int poff_tile = -1;
+  auto dma_patch = [&](int blk, int buf) __attribute__((always_inline)) {
+    const int j = blk / VB::NVB, vb = blk - (blk / VB::NVB) * VB::NVB;
+    if (j != poff_tile) {  // compile-time after unrolling (blk is a step constant)
+      tile_off(j, poff);
+      poff_tile = j;
+    }
+    const unsigned bo = (unsigned)(gx_boff<NCB, CF>(VB::pblk(vb)) * 2);
+#pragma unroll
+    for (int i = 0; i < PDMA; ++i) s2w_dma16(prs, poff[i] + bo, patch + buf * PATCHB + (i * NW + wid) * 1024);
   };
   // weights: ring row co holds output channel n0 + xperm(co) (16-byte epilogue)
   const _Float16* wsrc[WDMA];

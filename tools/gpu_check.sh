@@ -10,6 +10,8 @@
 #   ab:L,L:V,V      interleaved per-launch A/B in one process (tools/layer_ab.py), layers L, variants V
 #                   ($AB_ROUNDS rounds, $AB_ARGS extra, e.g. "--precision fp16x3")
 #   fwdab:L:V[,..]  interleaved whole-forward A/B (tools/head_ab.py --ab L:V ...)
+#   soab:A.so[,B.so] interleaved A/B of other builds of the library against the in-tree one
+#                   (tools/so_ab.py: one process per build and round; PERSEUS_AMD_LIB_AB)
 #   profile         rocprofv3 --kernel-trace --stats of the bench command + kernel traces of plain
 #                   fp16 / fp16x3 forwards + the factor path + FETCH_SIZE and WRITE_SIZE passes
 #                   (summarise here: tools/rocprof_summary.py --dir gpurun_out/$TAG --tag $TAG)
@@ -54,6 +56,11 @@ step() {
       (cd $R && timeout -k 10 300 $PY tools/layer_ab.py --variants ${V//,/ } --layers ${L//,/ } \
         --rounds ${AB_ROUNDS:-8} ${AB_ARGS}) >> $O/ab.log 2>&1
       local rc=$?; tail -4 $O/ab.log; return $rc ;;
+    soab:*)  # soab:OLD.so[,OLD2.so]: the in-tree build against other builds (tools/so_ab.py)
+      local libs=${s#soab:}
+      (cd $R && timeout -k 10 900 $PY tools/so_ab.py ${libs//,/ } perseus_amd/lib/libperseus_amd.so \
+        --rounds ${AB_ROUNDS:-6} ${AB_ARGS}) >> $O/soab.log 2>&1
+      local rc=$?; tail -25 $O/soab.log; return $rc ;;
     fwdab:*)
       local spec=${s#fwdab:}
       (cd $R && timeout -k 10 400 $PY tools/head_ab.py --ab ${spec//,/ } ${AB_ARGS}) >> $O/fwdab.log 2>&1
