@@ -331,7 +331,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int RL = PART ? 0 : XS * TN + ((EPI & EPI_RES) ? XS * TM * TN / 2 : 0);
   // epilogue loads (bias, residual) issued RSD steps before the end: early enough to
   // land, late enough not to hold their VGPRs across the whole K loop
-  constexpr int RSD = 4;
+  constexpr int RSD = NSTEPS >= 28 ? NSTEPS / 7 : 4;  // ~2 us before the end (layer4: 10 of 72 steps)
   constexpr GxPlan plan{NSTEPS, VB::NVB, PD, WDMA, PDMA, RL, NSTEPS > RSD ? NSTEPS - RSD : 0, G, 9, 0, 0, XM ? 1 : 0};
   constexpr int WSLOT = (XM ? 2 : 1) * WB;  // ring slot: one weight tile, or two (XM)
   static_assert(2 * PATCHB + NSLOT * WSLOT <= 163840, "LDS");

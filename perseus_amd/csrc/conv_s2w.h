@@ -56,8 +56,11 @@ struct S2wPlan {
   constexpr int before(int t) const { return t > 0 ? cum(t - 1) : 0; }
   // ops issued after the newest op the fragments of step v need (its weight tile, and the
   // region of its unit its taps read), counted at the end of step s
+  // The prologue issues unit 0's even rows, W(0 .. pd - 1), then unit 0's odd rows (po ops) and
+  // waits for all but those: the odd rows land during steps 0-3, which read only the even rows.
+  // Positions of prologue ops are <= 0: the even rows and prologue weights -po, the odd rows 0.
   constexpr int vm_after(int s, int v) const {
-    int need = 0;
+    int need = -po;  // prologue weights / even rows: the odd rows' po DMAs were issued after them
     if (v >= pd) {
       const int t = v - pd;
       need = before(t) + ns(t) + nw(t);
@@ -71,6 +74,8 @@ struct S2wPlan {
       const int t = u * 10;
       const int e = before(t) + ns(t) + nw(t) + npo(t);
       need = e > need ? e : need;
+    } else if (tv >= 4) {  // unit 0's odd rows: the newest prologue ops
+      need = 0 > need ? 0 : need;
     }
     const int n = cum(s) - need;
     return n < 0 ? 0 : (n > 63 ? 63 : n);
@@ -219,7 +224,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
       accd[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
-  // prologue: bias / bias2 of this workgroup's channels to LDS, unit 0's two regions, W(0 .. PD-1), drained
+  // prologue: bias / bias2 of this workgroup's channels to LDS, unit 0's even rows, W(0 .. PD-1), unit 0's
+  // odd rows; everything but the odd rows waited for
   if (tid < BN) {
     bl[tid] = a.bias[n0 + tid];
     bl[BN + tid] = a.bias2[n0 + tid];
@@ -229,12 +235,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_w(ConvS2Args a, int xg
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  dma_region(0, std::false_type{});
   dma_region(0, std::true_type{});
 #pragma unroll
   for (int t = 0; t < PD; ++t)
     if (t < NSTEPS) dma_w(t);
-  xwait_vm<0>();
+  dma_region(0, std::false_type{});  // odd rows last: needed from step 4 on (S2wPlan::vm_after)
+  xwait_vm<PO>();
   __builtin_amdgcn_s_barrier();
 
   _Float16* __restrict__ out = (_Float16*)a.out;
