@@ -113,6 +113,9 @@ int launch_stem_pool_x3_small(const float* x, int B, int Cin, const _Float16* w,
 int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s);
 // the same with LDS-DMA staging spread through the K loop (conv_c64d.hip)
 int launch_conv3x3_c64d(const ConvArgs& a, int variant, hipStream_t s);
+int launch_conv3x3_c64v(const ConvArgs& a, int variant, hipStream_t s);
+// CUs a launch on stream s may use (its CU mask, else the device's): persistent grids size by it
+int conv_stream_cus(hipStream_t s);
 
 
 template <typename T>

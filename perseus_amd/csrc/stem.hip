@@ -284,7 +284,11 @@ __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__
 // at pair j's barrier, 20 + j = wave 4 (moving) at pair j's barrier, 40 + j = wave 0 past it,
 // 60 = start, 61 = prologue barrier passed, 62 = wave 0 done, 63 = wave 4 done; 58 / 59 =
 // s_memtime (shader clock) at wave 0's start / end
-template <int PBT, int D, bool PRE = false, int DBG = 0>
+// XM (A/B): XCD-grouped bands -- workgroup L = blockIdx.y * gridDim.x + blockIdx.x runs on XCD
+// L % 8, so the plain (band, image) = (blockIdx.x, blockIdx.y) puts an image's bands on different
+// XCDs and the 7 halo input rows between two bands are fetched into two L2s; XM gives the bands of
+// one image to workgroups L, L + 8, ... (one XCD).  A bijection when B % 8 == 0, else the identity.
+template <int PBT, int D, bool PRE = false, int DBG = 0, bool XM = false>
 __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ x, int B, int Cin,
                                                       const _Float16* __restrict__ w, const float* __restrict__ bias,
                                                       _Float16* __restrict__ out, RgbdSrc src,
@@ -305,8 +309,15 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = lane >> 4, r16 = lane & 15;
-  const int n = blockIdx.y;
-  const int p0 = blockIdx.x * PBT;
+  int n = blockIdx.y, band = blockIdx.x;
+  if constexpr (XM) {
+    if (gridDim.y % 8 == 0) {
+      const int L = blockIdx.y * gridDim.x + blockIdx.x, m = L >> 3;
+      n = (m / (int)gridDim.x) * 8 + (L & 7);
+      band = m % (int)gridDim.x;
+    }
+  }
+  const int p0 = band * PBT;
   const bool mover = wid >= 4;
   const int mt = tid & 255;  // thread index within the role
   const float* xn = x + (size_t)n * Cin * 256 * 256;
@@ -556,11 +567,11 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
   }
 }
 
-template <int PBT, int D, bool PRE = false, int DBG = 0>
+template <int PBT, int D, bool PRE = false, int DBG = 0, bool XM = false>
 static int run_stem4(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out, hipStream_t s,
                      RgbdSrc src = RgbdSrc{}, unsigned long long* trace = nullptr) {
   PA_CHECK((size_t)B * 64 * 64 * 64 * 2 < 0x7fffffffu, "stem: output over 2 GB");
-  hipLaunchKernelGGL((stem_role_fp16<PBT, D, PRE, DBG>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out,
+  hipLaunchKernelGGL((stem_role_fp16<PBT, D, PRE, DBG, XM>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out,
                      src, trace);
   PA_LAUNCH_CHECK();
   return PA_OK;
@@ -616,6 +627,7 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     case 27: return run_stem4<8, 2>(x, B, Cin, w, bias, out, s);  // shorter bands at any batch (A/B)
     case 28: return run_stem4<4, 2>(x, B, Cin, w, bias, out, s);
     case 29: return run_stem4<32, 2>(x, B, Cin, w, bias, out, s);
+    case 30: return run_stem4<16, 2, false, 0, true>(x, B, Cin, w, bias, out, s);  // XCD-grouped bands
     // shipped: version 4, the role split (29.3 vs 31.8 us per B = 64 launch, bit-identical;
     // prefetch depth 3 / 4 measured 29.7 / 30.4 us)
     default: break;

@@ -15,6 +15,7 @@
 #   profile         rocprofv3 --kernel-trace --stats of the bench command + kernel traces of plain
 #                   fp16 / fp16x3 forwards + the factor path + FETCH_SIZE and WRITE_SIZE passes
 #                   (summarise here: tools/rocprof_summary.py --dir gpurun_out/$TAG --tag $TAG)
+#   fetch[:name]    FETCH_SIZE + WRITE_SIZE passes only (over pmc_forward.py $FWD_ARGS) -> name_fetch/, name_write/
 #   mfma            MFMA counter pass (summarise: tools/mfma_counters.py gpurun_out/$TAG --tag $TAG)
 #   sq              three SQ counter passes (summarise: tools/pmc_table.py gpurun_out/$TAG)
 #   stream          streaming bench (tools/streaming_bench.py $STREAM_ARGS)
@@ -75,6 +76,9 @@ step() {
       (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/fac_kt -o kt -- \
         $PY $R/tools/factor_prof.py) > $O/fac_kt.log 2>&1 && echo fac_kt_ok && \
       pmc fetch FETCH_SIZE && echo fetch_ok && pmc write WRITE_SIZE && echo write_ok ;;
+    fetch|fetch:*)
+      local nm=${s#fetch}; nm=${nm#:}
+      pmc ${nm:+${nm}_}fetch FETCH_SIZE && pmc ${nm:+${nm}_}write WRITE_SIZE && echo fetch_ok ;;
     mfma)
       pmc mfma SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE && echo mfma_ok ;;
     sq)

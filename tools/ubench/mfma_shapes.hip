@@ -8,7 +8,8 @@
 //   * 16x16x32 register-blocked 128x64 per wave (0.375 reads per MFMA), one wave per SIMD.
 // Each wave streams its fragments from a 64 KB LDS image (conflict-free 64 x 16 B rows),
 // READS = 0: operands stay in registers; 1: read right before use; 2: read one k-group
-// ahead (software pipelined, what the conv kernels do).  Random fp16 operands (clock
+// ahead (software pipelined, what the conv kernels do); 3: as 2 for the B (pixel) fragments
+// only, the A (weight) fragments stay in registers (round 5: weight-resident-in-VGPR layer1).  Random fp16 operands (clock
 // depends on data: MI355X_MICROARCH.md 'DVFS give-back').  Clock = s_memtime /
 // s_memrealtime x 100 MHz per wave, median.
 //
@@ -16,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <vector>
 
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(WAVES * 64) void k(const u4* __restrict__ in, float
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   const int base = lane + (tid >> 6) * 64 * 3;
   u4 ga[TN], gb[TM];
-  if (READS == 2) {
+  if (READS >= 2) {
 #pragma unroll
     for (int i = 0; i < TN; ++i) ga[i] = lds[(base + i * 256) & 4095];
 #pragma unroll
@@ -75,6 +77,13 @@ __global__ __launch_bounds__(WAVES * 64) void k(const u4* __restrict__ in, float
       for (int i = 0; i < TN; ++i) fa[i] = lds[(base + i * 256 + off) & 4095];
 #pragma unroll
       for (int i = 0; i < TM; ++i) fb[i] = lds[(base + 2048 + i * 256 + off) & 4095];
+    }
+    if (READS == 3) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        fb[i] = gb[i];
+        gb[i] = lds[(base + 2048 + i * 256 + off + 64) & 4095];
+      }
     }
     if (READS == 2) {
 #pragma unroll
@@ -132,7 +141,7 @@ void run(const char* name, const u4* in, float* out, unsigned long long* clk) {
   const double flop = mflop * TM * TN * (double)iters * grid * WAVES * reps;
   const double tf = flop / (ms * 1e-3) / 1e12;
   // reads per 16-cycle MFMA-equivalent (1024 FLOP/clk/SIMD either shape)
-  const double rpm = READS ? (double)(TM + TN) / (TM * TN) * (16.0 / S) : 0.0;
+  const double rpm = READS ? (double)(READS == 3 ? TM : TM + TN) / (TM * TN) * (16.0 / S) : 0.0;
   const double ghz_med = ghz[ghz.size() / 2];
   printf("%-44s %7.1f TF  %.3f of 2.5PF  %.3f of issue@clk  clk %.3f GHz  reads/16cyc %.3f\n", name, tf, tf / 2500.0,
          tf / (1024.0 * 4 * 256 * ghz_med * 1e-3), ghz_med, rpm);
@@ -153,6 +162,20 @@ int main() {
     v = (_Float16)(((int)(s >> 9) % 2001 - 1000) / 1000.0f);  // uniform [-1, 1]
   }
   hipMemcpy(in, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+  if (getenv("SHAPES_R5")) {  // round 5: weights in registers, pixels from LDS
+    for (int pass = 0; pass < 2; ++pass) {
+      printf("--- pass %d\n", pass);
+      run<16, 2, 4, 2, 8>("16x16x32 lds 32x64/wave pref, 8w (c64d now)", in, out, clk);
+      run<16, 4, 2, 3, 8>("16x16x32 A regs 64x32/wave, 8w", in, out, clk);
+      run<16, 2, 2, 3, 8>("16x16x32 A regs 32x32/wave, 8w", in, out, clk);
+      run<16, 4, 4, 3, 8>("16x16x32 A regs 64x64/wave, 8w", in, out, clk);
+      run<16, 4, 4, 3, 4>("16x16x32 A regs 64x64/wave, 4w", in, out, clk);
+      run<16, 8, 4, 3, 4>("16x16x32 A regs 128x64/wave, 4w", in, out, clk);
+      run<16, 2, 4, 3, 4>("16x16x32 A regs 32x64/wave, 4w", in, out, clk);
+      run<16, 4, 4, 0, 4>("16x16x32 regs 64x64/wave, 4w", in, out, clk);
+    }
+    return 0;
+  }
   for (int pass = 0; pass < 2; ++pass) {
     printf("--- pass %d\n", pass);
     run<16, 4, 2, 0, 8>("16x16x32 regs 64x32/wave, 8w", in, out, clk);
