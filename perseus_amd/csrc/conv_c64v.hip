@@ -7,7 +7,19 @@
 // its 32 channels' weights for all 576 K (18 groups x 2 fragments x 16 B per lane = 144 VGPRs)
 // for the whole launch: the K loop reads only the 4 pixel fragments of a group for its 8 MFMAs
 // (0.5 reads per MFMA, nothing for the weights).  tools/ubench/mfma_shapes.hip, 8 waves,
-// 16x16x32 (profiles/r05o_mfma_shapes_regs.txt): 0.60 of 2.5 PF against 0.49 for c64d's shape.
+// 16x16x32 (profiles/r05o_mfma_shapes_regs.txt): 0.60 of 2.5 PF against 0.49 for c64d's shape;
+// in the kernel a tile's K loop takes 2.3-2.5 us against c64d's 3.1 (r05r trace).
+//
+// Two workgroup shapes (TH = tile rows, 16 columns):
+//  * TH = 16: 8 waves, one workgroup per CU (conv_c64d's tile).  The trace shows where the K-loop
+//    gain goes: the younger wave of each SIMD loses arbitration to its partner, finishes the
+//    tile ~1.1 us later and runs alone meanwhile, and the hand-over barrier holds the older one
+//    (4.1 us per tile against 2.4 us of MFMA work per SIMD).
+//  * TH = 8: 4 waves (one per SIMD), TWO workgroups per CU.  A SIMD's two waves now belong to
+//    different workgroups with their own barriers and patch buffers, so neither waits for the
+//    other at a tile boundary and one's epilogue overlaps the other's MFMAs.  Costs: a 10 x 18
+//    patch per 128 pixels (1.41x halo reads against 1.27x), and the weights staged in two halves
+//    (each workgroup has ~68 KB of LDS).
 //
 // Patch layout: 144 bytes per pixel (8 data chunks of 16 B + 1 pad chunk), the chunk holding
 // input channels 32 h + 8 q .. + 7 at position 2 q + h.  A lane's fragment address is then
@@ -17,41 +29,61 @@
 // in 256.  Conflict-free for ds_read_b128's lane groups (MI355X_MICROARCH.md LDS table): with
 // the xfrag pixel order, a group's q = 0 lanes hit 16-byte bank quads 9 P mod 16 = the even (odd)
 // quads and its q = 1 lanes 9 P + 2 mod 16 = the odd (even) ones.  The LDS-DMA writes 64 x 16 B
-// contiguous per wave-instruction, so the pad chunks are DMA'd too (out-of-range offset: zeros):
-// 46 wave-DMAs per patch instead of 41.
+// contiguous per wave-instruction, so the pad chunks are DMA'd too (out-of-range offset: zeros).
 //
-// Same tile (16 x 16 pixels), double-buffered patch (next tile's in the first third of the K
-// loop), XCD-grouped tile order, lane -> pixel map and channel permutation as conv_c64d.hip;
-// each accumulator sums its MFMAs in the same order (tap 0..8, 32-channel halves) and the
-// epilogue is the same (bias, residual, ReLU in f32), so the output is bit-identical to
-// conv_c64d's.
+// Double-buffered patch (next tile's in the first third of the K loop), the residual tile by
+// LDS-DMA (not 16 VGPRs through the K loop), XCD-grouped tile order, lane -> pixel map and
+// channel permutation as conv_c64d.hip; each accumulator sums its MFMAs in the same order (tap
+// 0..8, 32-channel halves) and the epilogue is the same (bias, residual, ReLU in f32), so the
+// output is bit-identical to conv_c64d's.
 #include "conv_gx.h"
 
 namespace pa {
 
-namespace c64v {
-constexpr int TH = 16, TW = 16, PH = TH + 2, PW = TW + 2, NP = PH * PW;  // 324 patch pixels
-constexpr int NWAVE = 8;
-constexpr int PXB = 144;                // bytes per patch pixel (8 chunks + 1 pad)
-constexpr int PJ = (NP * 9 + 63) / 64;  // 46 patch wave-DMAs
-constexpr int PATCHB = PJ * 1024;
-constexpr int PDW = (PJ + NWAVE - 1) / NWAVE;  // 6 per wave (waves 6, 7: 5)
-static_assert(PJ == 46 && PDW == 6, "patch DMA split");
-constexpr int RESB = TH * TW * 128;  // residual tile (LDS-DMA, 4 per wave)
-static_assert(2 * PATCHB + RESB + 256 <= 160 * 1024, "LDS");
-}  // namespace c64v
+template <int TH>
+struct C64v {
+  static constexpr int TW = 16, PH = TH + 2, PW = TW + 2, NP = PH * PW;
+  static constexpr int NWAVE = TH / 2;                   // wave = 4 pixel rows x one channel half
+  static constexpr int PXB = 144;                        // bytes per patch pixel (8 chunks + 1 pad)
+  static constexpr int PJ = (NP * 9 + 63) / 64;          // patch wave-DMAs (46 / 26)
+  static constexpr int PATCHB = PJ * 1024;
+  static constexpr int PDW = (PJ + NWAVE - 1) / NWAVE;   // per wave (6 / 7), the last round partial
+  static constexpr int RESB = TH * TW * 128;             // residual tile
+  static constexpr int RDW = RESB / 1024 / NWAVE;        // residual DMAs per wave (4)
+  static constexpr int WROUND = TH == 16 ? 9 : 5;        // weight taps staged per round
+  // RP (one workgroup per CU only: LDS): the residual tile double-buffered and DMA'd one tile
+  // ahead with the patch, so the epilogue needs no barrier of its own.  LDS = [patch 0 | res 0 |
+  // patch 1 | res 1] (RP) or [patch 0 | patch 1 | res]; the weights are staged in the second half
+  static constexpr bool RP = TH == 16;
+  static constexpr int BSTR = RP ? PATCHB + RESB : PATCHB;  // buffer stride
+  static constexpr int SMEM = 2 * PATCHB + (RP ? 2 : 1) * RESB;
+  static_assert(RESB / 1024 % NWAVE == 0, "residual DMA split");
+  static_assert(SMEM - BSTR >= WROUND * 64 * 128, "weight staging in patch buffer 1 + residual tile(s)");
+  static_assert((SMEM + 256) * (TH == 16 ? 1 : 2) <= 160 * 1024, "LDS per CU");
+};
 
-template <int EPI>
-__global__ __launch_bounds__(512) void conv3x3_c64v(ConvArgs a, int ntiles) {
-  using namespace c64v;
+// DBG = 4 (timing only): s_memrealtime stamps into a.trace (0 start, 1 prologue landed; tile t:
+// 2 + 4 t start, 3 + 4 t K loop done and DMAs landed, 4 + 4 t stores issued, 5 + 4 t hand-over
+// barrier passed; 20 + 8 t + wave: that wave's K loop done, t < 5)
+template <int EPI, int TH, int DBG = 0>
+__global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntiles) {
+  using G = C64v<TH>;
+  constexpr int TW = G::TW, PW = G::PW, NP = G::NP, NWAVE = G::NWAVE, PXB = G::PXB, PJ = G::PJ;
+  constexpr int PATCHB = G::PATCHB, PDW = G::PDW, RDW = G::RDW, BSTR = G::BSTR;
+  constexpr bool RP = G::RP;
   constexpr int TM = 4, TN = 2;  // wave tile: 64 pixels (4 rows of 16) x 32 channels
-  __shared__ __attribute__((aligned(1024))) char patch[2 * PATCHB];
-  __shared__ __attribute__((aligned(1024))) char resl[RESB];
+  // [patch 0 | patch 1 | residual tile]; the weights pass through [patch 1 | residual] in the
+  // prologue, before either is first written
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  char* patch = smem;
+  auto resb = [&](int b) __attribute__((always_inline)) { return RP ? smem + b * BSTR + PATCHB : smem + 2 * PATCHB; };
+  char* wst = smem + BSTR;
   __shared__ __attribute__((aligned(16))) float bias_l[64];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, r16 = lane & 15;
-  const int wn = wid & 1, wm = wid >> 1;  // channel half, pixel quarter (rows 4 wm .. 4 wm + 3)
+  const int wn = wid & 1, wm = wid >> 1;  // channel half, pixel rows 4 wm .. 4 wm + 3
+  if constexpr (DBG == 4) trace_stamp(a.trace, 0);
   const int H = a.Hout, W = a.Wout;
   const _Float16* __restrict__ in = (const _Float16*)a.in;
   const _Float16* __restrict__ w = (const _Float16*)a.w;
@@ -74,37 +106,49 @@ __global__ __launch_bounds__(512) void conv3x3_c64v(ConvArgs a, int ntiles) {
     const int img = t / tpi, rem = t - img * tpi;
     return Org{img, (rem / tw_n) * TH - 1, (rem - (rem / tw_n) * tw_n) * TW - 1, on};
   };
-  // patch DMA i of this wave: LDS slot c = (i * 8 + wid) * 64 + lane (16-byte units) holds
-  // pixel c / 9, position c % 9 (8: pad), i.e. input channels 8 ((pos & 1) * 4 + (pos >> 1)) .. + 7
-  // (offsets computed at the DMA: six per tile, outside the MFMA-dense part of the loop)
-  // (lane laundered through an empty asm at each use: otherwise the loop-invariant per-DMA
-  // offsets are hoisted out of the tile loop and held in ~30 VGPRs next to the weights)
-  auto fresh_lane = [&]() __attribute__((always_inline)) {
-    int l = lane;
-    asm volatile("" : "+v"(l));
-    return l;
-  };
-  auto dma_patch = [&](int i, const Org& o, int buf) __attribute__((always_inline)) {
-    const int c = (i * NWAVE + wid) * 64 + fresh_lane();
+  // patch DMA i of this wave: LDS slot c = (i * NWAVE + wid) * 64 + lane (16-byte units) holds
+  // pixel p = c / 9 (row pr, column pc of the patch), position c % 9 (8: pad), i.e. input
+  // channels 8 ((pos & 1) * 4 + (pos >> 1)) .. + 7.  Per lane and DMA one packed word, computed
+  // once: bits 0-17 the byte offset from the patch origin, 18-22 pr, 23-27 pc, 28 pad / past the
+  // patch; a DMA is then two bit-field extracts, the halo test and one add on a wave-uniform
+  // tile base.  (Decoding c at every DMA cost ~25 VALU each, six per tile in the K loop: the
+  // timing-only variant without that arithmetic ran 3-4 us faster per launch, r05v.)
+  unsigned pk[PDW];
+#pragma unroll
+  for (int i = 0; i < PDW; ++i) {
+    const int c = (i * NWAVE + wid) * 64 + lane;
     const int p = c / 9, pos = c - p * 9;
-    const int pr = p / PW, pc = p - pr * PW;
-    const int h = o.h0 + pr, x = o.x0 + pc;
-    const bool ok = o.on && pos < 8 && p < NP && (unsigned)h < (unsigned)H && (unsigned)x < (unsigned)W;
-    const unsigned vo = ok ? (unsigned)((((o.img * H + h) * W + x) * 64 + ((pos & 1) * 4 + (pos >> 1)) * 8) * 2) : S2W_OOB;
-    s2w_dma16(rsrc, vo, patch + buf * PATCHB + (i * NWAVE + wid) * 1024);
+    const int pr = p < NP ? p / PW : 0, pc = p < NP ? p - (p / PW) * PW : 0;
+    const unsigned rel = (unsigned)(((pr * W + pc) * 64 + ((pos & 1) * 4 + (pos >> 1)) * 8) * 2);
+    pk[i] = (rel & 0x3ffffu) | ((unsigned)pr << 18) | ((unsigned)pc << 23) | ((pos >= 8 || p >= NP) ? 1u << 28 : 0u);
+  }
+  auto dma_patch = [&](int i, const Org& o, int buf) __attribute__((always_inline)) {
+    if constexpr (DBG == 7) {  // timing only: no offset arithmetic (wrong data)
+      s2w_dma16(rsrc, (unsigned)(lane * 16 + i * 1024), patch + buf * BSTR + (i * NWAVE + wid) * 1024);
+      return;
+    }
+    const unsigned v = pk[i];
+    const int pr = (int)((v >> 18) & 31u), pc = (int)((v >> 23) & 31u);
+    const unsigned tb = (unsigned)(((o.img * H + o.h0) * W + o.x0) * 128);  // wave-uniform (may wrap)
+    const bool ok = o.on && !(v >> 28) && (unsigned)(o.h0 + pr) < (unsigned)H && (unsigned)(o.x0 + pc) < (unsigned)W;
+    s2w_dma16(rsrc, ok ? tb + (v & 0x3ffffu) : S2W_OOB, patch + buf * BSTR + (i * NWAVE + wid) * 1024);
   };
   auto dma_one = [&](int i, const Org& o, int buf) __attribute__((always_inline)) {
     if (i < PDW - 1 || wid < PJ - (PDW - 1) * NWAVE) dma_patch(i, o, buf);  // wave-uniform
   };
-  // residual tile (EPI_RES) into LDS by DMA i = 0..3 of each wave: slot c -> tile pixel c >> 3,
-  // slot chunk c & 7 = logical chunk (c & 7) ^ (pixel & 7) (the epilogue's reads are then
-  // conflict-free); held in LDS, not in 16 VGPRs through the K loop
+  // residual tile (EPI_RES) by DMA i of each wave: slot c -> tile pixel c >> 3 = i * 8 NWAVE + m
+  // (m = 8 wid + lane / 8), slot chunk c & 7 = logical chunk (c & 7) ^ (pixel & 7) (the epilogue's
+  // reads are then conflict-free); DMA i adds i * NWAVE / 2 rows to DMA 0's per-lane offset
   const s2w_u4 rres = s2w_rsrc(a.res ? a.res : a.in, abytes);
-  auto dma_res = [&](int i, int img, int th0, int tw0) __attribute__((always_inline)) {
-    const int c = (i * NWAVE + wid) * 64 + fresh_lane();
-    const int px = c >> 3, lc = (c & 7) ^ (px & 7);
-    const unsigned vo = (unsigned)((((img * H + th0 + (px >> 4)) * W + tw0 + (px & 15)) * 64 + lc * 8) * 2);
-    s2w_dma16(rres, vo, resl + (i * NWAVE + wid) * 1024);
+  const int mres = 8 * wid + (lane >> 3);
+  const unsigned rrel = (unsigned)((((mres >> 4) * W + (mres & 15)) * 64 + (((lane & 7) ^ (mres & 7)) * 8)) * 2);
+  auto dma_res = [&](int i, int img, int th0, int tw0, int rb) __attribute__((always_inline)) {
+    if constexpr (DBG == 7) {
+      s2w_dma16(rres, (unsigned)(lane * 16 + i * 1024), resb(rb) + (i * NWAVE + wid) * 1024);
+      return;
+    }
+    const unsigned tb = (unsigned)((((img * H + th0 + i * (NWAVE / 2)) * W + tw0) * 128));
+    s2w_dma16(rres, tb + rrel, resb(rb) + (i * NWAVE + wid) * 1024);
   };
 
   const int o = xfrag(r16);
@@ -113,27 +157,53 @@ __global__ __launch_bounds__(512) void conv3x3_c64v(ConvArgs a, int ntiles) {
   if (tid < 64) bias_l[tid] = a.bias[tid];  // read back in the epilogue (8 VGPRs not held through the K loop)
   __builtin_amdgcn_sched_barrier(0);
 
-  // prologue: the first tile's patch, then this wave's weights into registers: fragment (K, tn) =
-  // channel xperm(32 wn + 16 tn + r16), tap K / 2, input channels 32 (K & 1) + 8 q .. + 7
+  // prologue: the first tile's patch; the weights by LDS-DMA (conv_c64d.hip's layout: row
+  // tap * 64 + rho holds channel xperm(rho), 16-byte chunks XOR-swizzled), once per workgroup, in
+  // rounds of WROUND taps; every wave reads its 36 fragments: (K, tn) = channel
+  // xperm(32 wn + 16 tn + r16), tap K / 2, input channels 32 (K & 1) + 8 q .. + 7.  (Loading them
+  // straight into VGPRs had the waves of a channel half fetch the same bytes from L2: 295 KB per
+  // workgroup, a 10 us prologue, r05q trace.)
   int j = blockIdx.x;
   {
     const Org o0 = origin(tmap(j), true);
 #pragma unroll
     for (int i = 0; i < PDW; ++i) dma_one(i, o0, 0);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  xu4 wr[18][TN];
-  {
-    const _Float16* ws0 = w + (size_t)xperm(wn * 32 + r16) * 576 + q * 8;
-    const _Float16* ws1 = w + (size_t)xperm(wn * 32 + 16 + r16) * 576 + q * 8;
+    if constexpr (RP && (EPI & EPI_RES)) {
 #pragma unroll
-    for (int k = 0; k < 18; ++k) {
-      wr[k][0] = *reinterpret_cast<const xu4*>(ws0 + (k >> 1) * 64 + (k & 1) * 32);
-      wr[k][1] = *reinterpret_cast<const xu4*>(ws1 + (k >> 1) * 64 + (k & 1) * 32);
+      for (int i = 0; i < RDW; ++i) dma_res(i, o0.img, o0.h0 + 1, o0.x0 + 1, 0);
     }
   }
-  xwait_vm<0>();  // patch + weights (the compiler's waitcnt pass sees this wait: no weight waits in the loop)
-  lds_barrier();
+  xu4 wr[18][TN];
+  {
+    constexpr int DPT = 8 / NWAVE;  // DMAs (8 rows of 128 B each) per wave per tap
+    static_assert(DPT * NWAVE * 1024 == 64 * 128, "weight DMA split");
+    auto stage = [&](auto t0c, auto t1c) __attribute__((always_inline)) {
+      constexpr int T0 = decltype(t0c)::value, T1 = decltype(t1c)::value;
+#pragma unroll
+      for (int tap = T0; tap < T1; ++tap)
+#pragma unroll
+        for (int d = 0; d < DPT; ++d) {
+          const int row0 = (d * NWAVE + wid) * 8 + (lane >> 3);  // row within the tap
+          const int lc = (lane & 7) ^ ((row0 >> 1) & 7);
+          xdma16(w + (size_t)xperm(row0) * 576 + tap * 64 + lc * 8, wst + ((tap - T0) * 8 + d * NWAVE + wid) * 1024);
+        }
+      xwait_vm<0>();
+      lds_barrier();
+#pragma unroll
+      for (int k = 2 * T0; k < 2 * T1; ++k)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          wr[k][tn] = *reinterpret_cast<const xu4*>(wst + xswz(((k >> 1) - T0) * 64 + wn * 32 + tn * 16 + r16, (k & 1) * 4 + q));
+      lds_barrier();  // reads retired before the staging area is rewritten
+    };
+    if constexpr (G::WROUND >= 9) {
+      stage(xic<0>{}, xic<9>{});
+    } else {
+      stage(xic<0>{}, xic<G::WROUND>{});
+      stage(xic<G::WROUND>{}, xic<9>{});
+    }
+  }
+  if constexpr (DBG == 4) trace_stamp(a.trace, 1);
 
   for (int t = 0; j < ntiles; ++t, j += gridDim.x) {
     const int buf = t & 1;
@@ -143,6 +213,7 @@ __global__ __launch_bounds__(512) void conv3x3_c64v(ConvArgs a, int ntiles) {
     const Org onext = origin(has_next ? tmap(next) : tile, has_next);
     const int img = tile / tpi, rem = tile - img * tpi;
     const int th0 = (rem / tw_n) * TH, tw0 = (rem - (rem / tw_n) * tw_n) * TW;
+    if constexpr (DBG == 4) trace_stamp(a.trace, 2 + 4 * t);
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -150,7 +221,7 @@ __global__ __launch_bounds__(512) void conv3x3_c64v(ConvArgs a, int ntiles) {
 #pragma unroll
       for (int k = 0; k < TN; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
     const __attribute__((address_space(3))) char* pb =
-        (const __attribute__((address_space(3))) char*)(size_t)(rbase + buf * PATCHB);
+        (const __attribute__((address_space(3))) char*)(size_t)(rbase + buf * BSTR);
     xu4 fb[2][TM];
     auto rd = [&](auto kc) __attribute__((always_inline)) {
       constexpr int K = decltype(kc)::value, TAP = K >> 1, HG = K & 1, S = K & 1;
@@ -172,19 +243,28 @@ __global__ __launch_bounds__(512) void conv3x3_c64v(ConvArgs a, int ntiles) {
     gx_for<0, 18>([&](auto kc) __attribute__((always_inline)) {
       constexpr int K = decltype(kc)::value;
       if constexpr (K + 1 < 18) rd(xic<K + 1>{});
+      __builtin_amdgcn_sched_barrier(0);  // next group's reads ahead of this group's MFMAs
       if constexpr (K < PDW) {  // next tile's patch, one DMA per group
         __builtin_amdgcn_sched_barrier(0);
         dma_one(K, onext, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr ((EPI & EPI_RES) && K < PDW + 4) {  // this tile's residual
+      } else if constexpr ((EPI & EPI_RES) && K < PDW + RDW) {  // this (RP: the next) tile's residual
         __builtin_amdgcn_sched_barrier(0);
-        dma_res(K - PDW, img, th0, tw0);
+        if constexpr (RP) {
+          if (has_next) dma_res(K - PDW, onext.img, onext.h0 + 1, onext.x0 + 1, buf ^ 1);
+        } else {
+          dma_res(K - PDW, img, th0, tw0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       mm(kc);
     });
     xwait_vm<0>();  // next patch (+ residual)
-    if constexpr (EPI & EPI_RES) lds_barrier();  // every wave's residual DMAs landed
+    if constexpr (DBG == 4) {  // (after the wait: a stamp's store would otherwise be waited for)
+      trace_stamp(a.trace, 3 + 4 * t);
+      if (lane == 0 && t < 5) a.trace[blockIdx.x * TRACE_SLOTS + 20 + 8 * t + wid] = __builtin_amdgcn_s_memrealtime();
+    }
+    if constexpr (!RP && (EPI & EPI_RES)) lds_barrier();  // every wave's residual DMAs landed
 
     _Float16* __restrict__ out = (_Float16*)a.out;
     f32x4 bias[TN];
@@ -194,7 +274,7 @@ __global__ __launch_bounds__(512) void conv3x3_c64v(ConvArgs a, int ntiles) {
     for (int tm = 0; tm < TM; ++tm) {
       const int px = (wm * 4 + tm) * TW + o;  // tile pixel
       half8 rv;
-      if constexpr (EPI & EPI_RES) rv = *reinterpret_cast<const half8*>(resl + px * 128 + (((wn * 4 + q) ^ (px & 7)) << 4));
+      if constexpr (EPI & EPI_RES) rv = *reinterpret_cast<const half8*>(resb(buf) + px * 128 + (((wn * 4 + q) ^ (px & 7)) << 4));
       half8 hv;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -205,28 +285,48 @@ __global__ __launch_bounds__(512) void conv3x3_c64v(ConvArgs a, int ntiles) {
       const unsigned ob = (unsigned)((((img * H + th0 + wm * 4 + tm) * W + tw0 + o) * 64 + wn * 32 + q * 8) * 2);
       store16<true>(out, ob, hv);
     }
-    // every wave's DMAs into buf ^ 1 landed (its wait above) and its reads of buf retired
+    if constexpr (DBG == 4) trace_stamp(a.trace, 4 + 4 * t);
+    // every wave's DMAs into buf ^ 1 landed (its wait above) and its reads of buf (and of the
+    // residual tile) retired
     lds_barrier();
+    if constexpr (DBG == 4) trace_stamp(a.trace, 5 + 4 * t);
+  }
+  if constexpr (DBG == 4) {
+    __builtin_amdgcn_s_waitcnt(0);
+    trace_stamp(a.trace, 63);
   }
 }
 
+template <int TH, int DBG>
+static int run_c64v(const ConvArgs& a, hipStream_t s) {
+  PA_CHECK(a.Hout % TH == 0 && a.Wout % 16 == 0, "c64v conv: %dx%d not tiled by %dx16", a.Hout, a.Wout, TH);
+  const int tiles = a.B * (a.Hout / TH) * (a.Wout / 16);
+  const int slots = conv_stream_cus(s) * (TH == 16 ? 1 : 2);  // resident workgroups
+  const int grid = tiles < slots ? tiles : slots;
+  if (a.epi & EPI_RES)
+    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES, TH, DBG>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
+  else
+    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU, TH, DBG>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
+  PA_LAUNCH_CHECK();
+  return PA_OK;
+}
+
+// variant: 0 = 16-row tiles, one 8-wave workgroup per CU; 1 = 8-row tiles, two 4-wave
+// workgroups per CU; 4 / 6 = their s_memrealtime traces; 7 / 8 = timing only (wrong data): the
+// DMAs without their offset arithmetic
 int launch_conv3x3_c64v(const ConvArgs& a, int variant, hipStream_t s) {
   PA_CHECK(a.Cin == 64 && a.Cout == 64 && a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout,
            "c64v conv: Cin=Cout=64 stride-1 only");
-  PA_CHECK(a.Hout % c64v::TH == 0 && a.Wout % c64v::TW == 0, "c64v conv: %dx%d not tiled by 16x16", a.Hout, a.Wout);
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES), "c64v conv: epilogue %d", a.epi);
   PA_CHECK((size_t)a.B * a.Hout * a.Wout * 64 * 2 < 0x7fffffffu, "c64v conv: output over 2 GB");
-  (void)variant;
+  PA_CHECK(a.Wout <= 96, "c64v conv: width %d (packed patch offsets: 18 bits)", a.Wout);
   if (a.B <= 0) return PA_OK;
-  const int tiles = a.B * (a.Hout / c64v::TH) * (a.Wout / c64v::TW);
-  const int cus = conv_stream_cus(s);
-  const int grid = tiles < cus ? tiles : cus;
-  if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES>), dim3(grid), dim3(512), 0, s, a, tiles);
-  else
-    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU>), dim3(grid), dim3(512), 0, s, a, tiles);
-  PA_LAUNCH_CHECK();
-  return PA_OK;
+  if (variant == 4 && a.trace) return run_c64v<16, 4>(a, s);
+  if (variant == 6 && a.trace) return run_c64v<8, 4>(a, s);
+  if (variant == 1) return run_c64v<8, 0>(a, s);
+  if (variant == 7) return run_c64v<16, 7>(a, s);  // timing only: DMA offsets without arithmetic
+  if (variant == 8) return run_c64v<8, 7>(a, s);
+  return run_c64v<16, 0>(a, s);
 }
 
 }  // namespace pa
