@@ -127,6 +127,8 @@ def main():
     model = KeypointCNN(num_channels=4, precision=args.precision)
     model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
     model.eval()
+    if os.environ.get("PERSEUS_AMD_BENCH_VARIANTS"):  # A/B of kernel variants (tools/gpu_check.sh benchab)
+        model.set_variants(dict(tuple(int(t) for t in lv.split(":")) for lv in os.environ["PERSEUS_AMD_BENCH_VARIANTS"].split(",")))
     # this rank's frame shard, resident in HBM before timing
     x_host = synth.synthetic_frames(args.seed, B, first=rank * B)
     x = torch.from_numpy(x_host).to(dev)

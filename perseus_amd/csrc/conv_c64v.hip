@@ -129,6 +129,13 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
     }
     const unsigned v = pk[i];
     const int pr = (int)((v >> 18) & 31u), pc = (int)((v >> 23) & 31u);
+    if constexpr (DBG == 8) {  // timing only: the real arithmetic on every tile's origin = tile 1's (L2-hot data)
+      const Org o1{0, -1, 15, true};
+      const unsigned tb = (unsigned)(((o1.img * H + o1.h0) * W + o1.x0) * 128) + (unsigned)(o.img & 0);
+      const bool ok = o1.on && !(v >> 28) && (unsigned)(o1.h0 + pr) < (unsigned)H && (unsigned)(o1.x0 + pc) < (unsigned)W;
+      s2w_dma16(rsrc, ok ? tb + (v & 0x3ffffu) : S2W_OOB, patch + buf * BSTR + (i * NWAVE + wid) * 1024);
+      return;
+    }
     const unsigned tb = (unsigned)(((o.img * H + o.h0) * W + o.x0) * 128);  // wave-uniform (may wrap)
     const bool ok = o.on && !(v >> 28) && (unsigned)(o.h0 + pr) < (unsigned)H && (unsigned)(o.x0 + pc) < (unsigned)W;
     s2w_dma16(rsrc, ok ? tb + (v & 0x3ffffu) : S2W_OOB, patch + buf * BSTR + (i * NWAVE + wid) * 1024);
@@ -324,8 +331,10 @@ int launch_conv3x3_c64v(const ConvArgs& a, int variant, hipStream_t s) {
   if (variant == 4 && a.trace) return run_c64v<16, 4>(a, s);
   if (variant == 6 && a.trace) return run_c64v<8, 4>(a, s);
   if (variant == 1) return run_c64v<8, 0>(a, s);
+  if (variant == 2) return (a.epi & EPI_RES) ? run_c64v<8, 0>(a, s) : run_c64v<16, 0>(a, s);
   if (variant == 7) return run_c64v<16, 7>(a, s);  // timing only: DMA offsets without arithmetic
   if (variant == 8) return run_c64v<8, 7>(a, s);
+  if (variant == 9) return run_c64v<16, 8>(a, s);  // timing only: every patch DMA reads tile 1's patch
   return run_c64v<16, 0>(a, s);
 }
 

@@ -429,9 +429,10 @@ def test_kernel_variants_agree_bit_for_bit(B):
         (((1, 32),), y0),  # layer1: the one-tile patch kernel (independent of the shipped LDS-DMA kernel)
         (((7, 3),), y0),  # avgpool + fc fused into layer4's last conv instead of head_fp16
         (((0, 16),), y0),  # stem: version 3 (every wave convolves and moves rows) vs the shipped role split
-        (((1, 80),), y0),  # layer1: weights resident in VGPRs (conv_c64v.hip)
-        (((1, 81),), y0),  # layer1: weights in VGPRs, 8-row tiles, two 4-wave workgroups per CU
-        (((0, 30), (1, 69)), y0),  # stem bands in XCD-grouped order; layer1 tiles in the plain order (same arithmetic per tile)
+        (((1, 60),), y0),  # layer1: conv_c64d.hip (weights resident in LDS; shipped until round 5)
+        (((1, 80),), y0),  # layer1: conv_c64v.hip 16-row tiles on every conv
+        (((1, 81),), y0),  # layer1: conv_c64v.hip 8-row tiles, two 4-wave workgroups per CU, on every conv
+        (((0, 30), (1, 69)), y0),  # stem bands in XCD-grouped order; conv_c64d tiles in the plain order (same arithmetic)
         (((6, 41),), y0),  # conv_s2w: layer2 one tile per workgroup, layer3 prefetch distance 2
         (((6, 42),), y0),  # conv_s2w: layer2 prefetch distance 2
         (((6, 44),), y0),  # conv_s2w: XCD-aware order off

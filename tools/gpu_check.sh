@@ -10,6 +10,8 @@
 #   ab:L,L:V,V      interleaved per-launch A/B in one process (tools/layer_ab.py), layers L, variants V
 #                   ($AB_ROUNDS rounds, $AB_ARGS extra, e.g. "--precision fp16x3")
 #   fwdab:L:V[,..]  interleaved whole-forward A/B (tools/head_ab.py --ab L:V ...)
+#   benchab:L:V[,L:V] the driver's bench command, shipped and with the variants
+#                   (PERSEUS_AMD_BENCH_VARIANTS), alternated $BENCHAB_PAIRS times -> benchab.jsonl
 #   soab:A.so[,B.so] interleaved A/B of other builds of the library against the in-tree one
 #                   (tools/so_ab.py: one process per build and round; PERSEUS_AMD_LIB_AB)
 #   profile         rocprofv3 --kernel-trace --stats of the bench command + kernel traces of plain
@@ -66,6 +68,15 @@ step() {
       local spec=${s#fwdab:}
       (cd $R && timeout -k 10 400 $PY tools/head_ab.py --ab ${spec//,/ } ${AB_ARGS}) >> $O/fwdab.log 2>&1
       local rc=$?; tail -4 $O/fwdab.log; return $rc ;;
+    benchab:*)
+      local vs=${s#benchab:}
+      for k in $(seq ${BENCHAB_PAIRS:-2}); do
+        (cd $R && timeout -k 10 400 $PY bench.py --gpus 1 --steps 20 --warmup 5 --no-streaming) 2>>$O/benchab.err | \
+          sed 's/^/{"ab": "shipped", "line": /; s/$/}/' >> $O/benchab.jsonl || return 1
+        (cd $R && PERSEUS_AMD_BENCH_VARIANTS=$vs timeout -k 10 400 $PY bench.py --gpus 1 --steps 20 --warmup 5 \
+          --no-streaming) 2>>$O/benchab.err | sed "s/^/{\"ab\": \"$vs\", \"line\": /; s/\$/}/" >> $O/benchab.jsonl || return 1
+        echo "pair $k done"
+      done ;;
     profile)
       (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/bench_kt -o kt -- \
         $PY $R/bench.py ${BENCH_ARGS}) > $O/bench.log 2>&1 && echo bench_kt_ok && \
