@@ -65,7 +65,13 @@ struct C64v {
 // DBG = 4 (timing only): s_memrealtime stamps into a.trace (0 start, 1 prologue landed; tile t:
 // 2 + 4 t start, 3 + 4 t K loop done and DMAs landed, 4 + 4 t stores issued, 5 + 4 t hand-over
 // barrier passed; 20 + 8 t + wave: that wave's K loop done, t < 5)
-template <int EPI, int TH, int DBG = 0>
+// DYN: tiles after the first are taken from a per-XCD counter (a.cnt[x], x = blockIdx.x % 8;
+// a.cnt[8] counts finished workgroups, and the last one zeroes all nine, so the counters are zero
+// between launches and across graph replays).  With two workgroups per CU the one that wins
+// arbitration on every SIMD runs ~30 % faster than its partner; with a static 4 tiles each the
+// launch ended ~3 us after the median workgroup (r05u trace), with stolen tiles it takes more.
+// The next tile's index is fetched one tile ahead (its patch is DMA'd during the current one).
+template <int EPI, int TH, int DBG = 0, bool DYN = false>
 __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntiles) {
   using G = C64v<TH>;
   constexpr int TW = G::TW, PW = G::PW, NP = G::NP, NWAVE = G::NWAVE, PXB = G::PXB, PJ = G::PJ;
@@ -113,18 +119,37 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   // patch; a DMA is then two bit-field extracts, the halo test and one add on a wave-uniform
   // tile base.  (Decoding c at every DMA cost ~25 VALU each, six per tile in the K loop: the
   // timing-only variant without that arithmetic ran 3-4 us faster per launch, r05v.)
-  unsigned pk[PDW];
+  // (DYN, short of VGPRs for the tile fetch: two DMAs per word, 16 bits each = pr | pc << 5 |
+  // pos << 10 | pad << 14, the offset recomputed at the DMA)
+  constexpr int NPK = DYN ? (PDW + 1) / 2 : PDW;
+  unsigned pk[NPK];
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) pk[i] = 0;
 #pragma unroll
   for (int i = 0; i < PDW; ++i) {
     const int c = (i * NWAVE + wid) * 64 + lane;
     const int p = c / 9, pos = c - p * 9;
     const int pr = p < NP ? p / PW : 0, pc = p < NP ? p - (p / PW) * PW : 0;
-    const unsigned rel = (unsigned)(((pr * W + pc) * 64 + ((pos & 1) * 4 + (pos >> 1)) * 8) * 2);
-    pk[i] = (rel & 0x3ffffu) | ((unsigned)pr << 18) | ((unsigned)pc << 23) | ((pos >= 8 || p >= NP) ? 1u << 28 : 0u);
+    const unsigned bad = (pos >= 8 || p >= NP) ? 1u : 0u;
+    if constexpr (DYN) {
+      pk[i >> 1] |= ((unsigned)pr | ((unsigned)pc << 5) | ((unsigned)(pos & 15) << 10) | (bad << 14)) << (16 * (i & 1));
+    } else {
+      const unsigned rel = (unsigned)(((pr * W + pc) * 64 + ((pos & 1) * 4 + (pos >> 1)) * 8) * 2);
+      pk[i] = (rel & 0x3ffffu) | ((unsigned)pr << 18) | ((unsigned)pc << 23) | (bad << 28);
+    }
   }
   auto dma_patch = [&](int i, const Org& o, int buf) __attribute__((always_inline)) {
     if constexpr (DBG == 7) {  // timing only: no offset arithmetic (wrong data)
       s2w_dma16(rsrc, (unsigned)(lane * 16 + i * 1024), patch + buf * BSTR + (i * NWAVE + wid) * 1024);
+      return;
+    }
+    if constexpr (DYN) {
+      const unsigned f = (pk[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      const int pr = (int)(f & 31u), pc = (int)((f >> 5) & 31u), pos = (int)((f >> 10) & 15u);
+      const unsigned tb = (unsigned)(((o.img * H + o.h0) * W + o.x0) * 128);
+      const unsigned rel = (unsigned)(((pr * W + pc) * 64 + ((pos & 1) * 4 + (pos >> 1)) * 8) * 2);
+      const bool ok = o.on && !(f >> 14) && (unsigned)(o.h0 + pr) < (unsigned)H && (unsigned)(o.x0 + pc) < (unsigned)W;
+      s2w_dma16(rsrc, ok ? tb + rel : S2W_OOB, patch + buf * BSTR + (i * NWAVE + wid) * 1024);
       return;
     }
     const unsigned v = pk[i];
@@ -171,6 +196,12 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   // straight into VGPRs had the waves of a channel half fetch the same bytes from L2: 295 KB per
   // workgroup, a 10 us prologue, r05q trace.)
   int j = blockIdx.x;
+  __shared__ int jnext_l;
+  const int x8 = blockIdx.x & 7;
+  auto jof = [&](unsigned k) __attribute__((always_inline)) { return (int)gridDim.x + 8 * (int)k + x8; };
+  if constexpr (DYN) {
+    if (tid == 0) jnext_l = jof(atomicAdd(a.cnt + x8, 1u));  // read after the prologue's barriers
+  }
   {
     const Org o0 = origin(tmap(j), true);
 #pragma unroll
@@ -212,10 +243,13 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   }
   if constexpr (DBG == 4) trace_stamp(a.trace, 1);
 
-  for (int t = 0; j < ntiles; ++t, j += gridDim.x) {
+  int jn = DYN ? 0 : j + (int)gridDim.x;
+  if constexpr (DYN) jn = __builtin_amdgcn_readfirstlane(jnext_l);
+  unsigned kdyn = 0;
+  for (int t = 0; j < ntiles; ++t) {
     const int buf = t & 1;
     const int tile = tmap(j);
-    const int next = j + gridDim.x;
+    const int next = jn;
     const bool has_next = next < ntiles;
     const Org onext = origin(has_next ? tmap(next) : tile, has_next);
     const int img = tile / tpi, rem = tile - img * tpi;
@@ -246,6 +280,9 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, wr[K][tn]),
                                                                __builtin_bit_cast(half8, fb[S][tm]), acc[tm][tn], 0, 0, 0);
     };
+    if constexpr (DYN) {  // the tile after next (its return is first used after the K loop's wait)
+      if (tid == 0 && has_next) kdyn = atomicAdd(a.cnt + x8, 1u);
+    }
     rd(xic<0>{});
     gx_for<0, 18>([&](auto kc) __attribute__((always_inline)) {
       constexpr int K = decltype(kc)::value;
@@ -266,7 +303,10 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
       }
       mm(kc);
     });
-    xwait_vm<0>();  // next patch (+ residual)
+    xwait_vm<0>();  // next patch (+ residual, + the dynamic fetch)
+    if constexpr (DYN) {
+      if (tid == 0) jnext_l = has_next ? jof(kdyn) : ntiles;  // read after the hand-over barrier
+    }
     if constexpr (DBG == 4) {  // (after the wait: a stamp's store would otherwise be waited for)
       trace_stamp(a.trace, 3 + 4 * t);
       if (lane == 0 && t < 5) a.trace[blockIdx.x * TRACE_SLOTS + 20 + 8 * t + wid] = __builtin_amdgcn_s_memrealtime();
@@ -297,6 +337,18 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
     // residual tile) retired
     lds_barrier();
     if constexpr (DBG == 4) trace_stamp(a.trace, 5 + 4 * t);
+    j = jn;
+    if constexpr (DYN) {
+      jn = __builtin_amdgcn_readfirstlane(jnext_l);
+    } else {
+      jn = j + (int)gridDim.x;
+    }
+  }
+  if constexpr (DYN) {  // the last workgroup out zeroes the counters (vector atomics)
+    if (tid == 0 && atomicAdd(a.cnt + 8, 1u) == gridDim.x - 1) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) atomicExch(a.cnt + i, 0u);
+    }
   }
   if constexpr (DBG == 4) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -304,16 +356,17 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   }
 }
 
-template <int TH, int DBG>
+template <int TH, int DBG, bool DYN = false>
 static int run_c64v(const ConvArgs& a, hipStream_t s) {
+  PA_CHECK(!DYN || a.cnt, "c64v conv: dynamic tiles need the handle's counters");
   PA_CHECK(a.Hout % TH == 0 && a.Wout % 16 == 0, "c64v conv: %dx%d not tiled by %dx16", a.Hout, a.Wout, TH);
   const int tiles = a.B * (a.Hout / TH) * (a.Wout / 16);
   const int slots = conv_stream_cus(s) * (TH == 16 ? 1 : 2);  // resident workgroups
   const int grid = tiles < slots ? tiles : slots;
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES, TH, DBG>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES, TH, DBG, DYN>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
   else
-    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU, TH, DBG>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU, TH, DBG, DYN>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -332,6 +385,8 @@ int launch_conv3x3_c64v(const ConvArgs& a, int variant, hipStream_t s) {
   if (variant == 6 && a.trace) return run_c64v<8, 4>(a, s);
   if (variant == 1) return run_c64v<8, 0>(a, s);
   if (variant == 2) return (a.epi & EPI_RES) ? run_c64v<8, 0>(a, s) : run_c64v<16, 0>(a, s);
+  if (variant == 3) return run_c64v<8, 0, true>(a, s);
+  if (variant == 5) return (a.epi & EPI_RES) ? run_c64v<8, 0, true>(a, s) : run_c64v<16, 0>(a, s);
   if (variant == 7) return run_c64v<16, 7>(a, s);  // timing only: DMA offsets without arithmetic
   if (variant == 8) return run_c64v<8, 7>(a, s);
   if (variant == 9) return run_c64v<16, 8>(a, s);  // timing only: every patch DMA reads tile 1's patch

@@ -55,6 +55,7 @@ struct pa_detector {
   size_t ws_bytes = 0;
   float* pool = nullptr;     // fused head: pooled means [cap][512] f32
   unsigned* cnt = nullptr;   // fused head: per-image-pair arrival counters, zero between launches
+  unsigned* tctr = nullptr;  // layer1 dynamic tile counters (conv_c64v.hip DYN), zero between launches
   int head_cap = 0;          // batch capacity of pool / cnt
   double flops_per_frame = 0;
   int device = 0;
@@ -196,6 +197,10 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
   PA_HIP(hipMemcpy(d->w3, h3.data(), h3.size() * sizeof(_Float16), hipMemcpyHostToDevice));
   PA_HIP(hipMemcpy(d->scl, hs.data(), hs.size() * sizeof(float), hipMemcpyHostToDevice));
   PA_HIP(hipMemcpy(d->bstem3, hbs.data(), hbs.size() * sizeof(float), hipMemcpyHostToDevice));
+  if (!d->tctr) {
+    PA_HIP(hipMalloc(&d->tctr, 64 * sizeof(unsigned)));
+    PA_HIP(hipMemset(d->tctr, 0, 64 * sizeof(unsigned)));
+  }
   return PA_OK;
 }
 
@@ -342,6 +347,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   auto trace = [&]() { return g_trace ? g_trace + (size_t)TRACE_LAUNCH * launch++ : nullptr; };
   // stride-1 convs: split-K form for small batches (pa_detector_set_split_k, conv_splitk.hip)
   auto conv_s1 = [&](ConvArgs& a, const char** kn) -> int {
+    if (!(a.epi & EPI_HEAD)) a.cnt = d->tctr;  // (only conv_c64v.hip reads it)
     if constexpr (std::is_same<T, _Float16>::value) {
       const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : a.Hout == 8 ? 4 : 0;
       // g_variant[layer] == 71 (A/B): layer2 split as well, layer1 on the persistent kernel
@@ -755,6 +761,7 @@ void pa_detector_destroy(pa_detector* d) {
   if (d->ws) hipFree(d->ws);
   if (d->pool) hipFree(d->pool);
   if (d->cnt) hipFree(d->cnt);
+  if (d->tctr) hipFree(d->tctr);
   if (d->part) hipFree(d->part);
   if (d->xin) hipFree(d->xin);
   delete d;

@@ -432,6 +432,7 @@ def test_kernel_variants_agree_bit_for_bit(B):
         (((1, 60),), y0),  # layer1: conv_c64d.hip (weights resident in LDS; shipped until round 5)
         (((1, 80),), y0),  # layer1: conv_c64v.hip 16-row tiles on every conv
         (((1, 81),), y0),  # layer1: conv_c64v.hip 8-row tiles, two 4-wave workgroups per CU, on every conv
+        (((1, 83),), y0),  # layer1: conv_c64v.hip 8-row tiles, tiles after the first from per-XCD counters
         (((0, 30), (1, 69)), y0),  # stem bands in XCD-grouped order; conv_c64d tiles in the plain order (same arithmetic)
         (((6, 41),), y0),  # conv_s2w: layer2 one tile per workgroup, layer3 prefetch distance 2
         (((6, 42),), y0),  # conv_s2w: layer2 prefetch distance 2

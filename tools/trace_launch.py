@@ -50,6 +50,12 @@ def main():
         tl = tl[wg]
         t0 = tl[:, 0].min()
         print(f"launch {li}: {len(wg)} workgroups; end-of-kernel max {(tl[:, 63].max() - t0) / 100:.2f} us")
+        if tl[:, 63].any():  # end time by dispatch half (which workgroups win arbitration)
+            h = len(wg) // 2
+            e = (tl[:, 63] - t0) / 100.0
+            print(f"  end by half: first {np.median(e[:h]):.2f} (max {e[:h].max():.2f})  "
+                  f"second {np.median(e[h:]):.2f} (max {e[h:].max():.2f}); by parity: even {np.median(e[0::2]):.2f} "
+                  f"odd {np.median(e[1::2]):.2f}")
         for s in range(64):
             col = tl[:, s]
             if not col.any():
