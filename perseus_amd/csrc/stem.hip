@@ -288,7 +288,15 @@ __global__ __launch_bounds__(512) void stem_pool3_fp16(const float* __restrict__
 // L % 8, so the plain (band, image) = (blockIdx.x, blockIdx.y) puts an image's bands on different
 // XCDs and the 7 halo input rows between two bands are fetched into two L2s; XM gives the bands of
 // one image to workgroups L, L + 8, ... (one XCD).  A bijection when B % 8 == 0, else the identity.
-template <int PBT, int D, bool PRE = false, int DBG = 0, bool XM = false>
+// BR (A/B): the bias in 16 VGPRs as the first tap row's MFMA accumulator input, instead of
+// 16 LDS reads per pair into the accumulators (same sum order: bias, then kh = 0..6)
+// IL (A/B): column tile 0's epilogue (per 16-channel group: 4 packed converts, 3 packed maxes, a
+// V-row write) interleaved in program order between tile 1's tap rows 1..4, one group each, instead
+// of after all of tile 1's MFMAs (an in-order wave issues its 56 MFMAs first, so the epilogue
+// behind them barely overlapped the pipe)
+// (BR and IL shipped this round: 27.3 vs 28.1 us per B = 64 launch, bit-identical, profiles/r05zl_stem_ab.log;
+// variant 0:34 is the previous form)
+template <int PBT, int D, bool PRE = false, int DBG = 0, bool XM = false, bool BR = true, bool IL = true>
 __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ x, int B, int Cin,
                                                       const _Float16* __restrict__ w, const float* __restrict__ bias,
                                                       _Float16* __restrict__ out, RgbdSrc src,
@@ -452,6 +460,9 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) wf[kh][tn] = *reinterpret_cast<const su32x4*>(wst + (kh * 4 + tn) * 1024 + lane * 16);
     half4 prev[2][TN];  // post-ReLU conv row 2p - 1, per column tile
+    f32x4 breg[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) breg[tn] = BR ? *reinterpret_cast<const f32x4*>(bl + tn * 16 + q * 4) : f32x4{};
     stem_for<0, PBT + 1>([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       const int r0 = 2 * p0 - 2 + 2 * j;  // pair j: conv rows r0 = 2p, r0 + 1 (p = p0 - 1 + j)
@@ -459,11 +470,13 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
       // column tile c = 0's epilogue (V write) is placed after c = 1's MFMAs are issued, so
       // its VALU work fills the MFMA pipe's shadow instead of following it
       f32x4 acc[2][2][TN];  // [column tile c][row t][tn]
-      auto conv_tile = [&](int c) __attribute__((always_inline)) {
+      auto conv_tile = [&](int c, auto&& hook) __attribute__((always_inline)) {
+        if constexpr (!BR) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int b = 0; b < TN; ++b) acc[c][t][b] = *reinterpret_cast<const f32x4*>(bl + b * 16 + q * 4);
+            for (int b = 0; b < TN; ++b) acc[c][t][b] = *reinterpret_cast<const f32x4*>(bl + b * 16 + q * 4);
+        }
         // the 9 input rows of this pair (row t + kh for conv row t, tap row kh), each read
         // once and four taps' MFMAs (two tap rows) ahead of its first use
         su32x4 fr[9];
@@ -479,13 +492,14 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
           // keep each read two tap rows ahead (the scheduler sank them); VALU / SALU / MFMA may
           // still cross, so the first column tile's epilogue can fill the second tile's MFMA shadow
           __builtin_amdgcn_sched_barrier(0x000E);
+          hook(kh);
 #pragma unroll
           for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int tn = 0; tn < TN; ++tn)
               acc[c][t][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, wf[kh][tn]),
-                                                                     __builtin_bit_cast(half8, fr[kh + 2 * t]), acc[c][t][tn],
-                                                                     0, 0, 0);
+                                                                     __builtin_bit_cast(half8, fr[kh + 2 * t]),
+                                                                     (BR && kh == 0) ? breg[tn] : acc[c][t][tn], 0, 0, 0);
         }
       };
       // rows above the image (only the whole pair r0 = -2, -1 of the first band) are 0 =
@@ -494,37 +508,45 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
       // max(prev, v0, max(v1, 0)) on the raw fp16 conv values, and prev (row 2p + 1) is kept
       // raw as well -- the same fp16 values as ReLU-then-max, one packed max fewer per pair of
       // channels
-      auto epi_tile = [&](int c) __attribute__((always_inline)) {
+      // one 16-channel group tn of column tile c (the same operations, per group, as before)
+      auto epi_tn = [&](int c, int tn) __attribute__((always_inline)) {
         const half4 z4 = half4{0, 0, 0, 0};
-        half4 v0[TN], v1[TN];
+        half4 v0, v1;
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v0[tn][e] = (_Float16)acc[c][0][tn][e];
-            v1[tn][e] = (_Float16)acc[c][1][tn][e];
-          }
-          if constexpr (j == 0) {
-            if (r0 < 0) v1[tn] = z4;
-          }
+        for (int e = 0; e < 4; ++e) {
+          v0[e] = (_Float16)acc[c][0][tn][e];
+          v1[e] = (_Float16)acc[c][1][tn][e];
+        }
+        if constexpr (j == 0) {
+          if (r0 < 0) v1 = z4;
         }
         if constexpr (j >= 1) {
           char* vw = vring + (j & 1) * CROWB;
           const int wo = wid * 32 + c * 16 + r16;
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn) {
-            const half4 vv = __builtin_elementwise_max(__builtin_elementwise_max(prev[c][tn], v0[tn]),
-                                                       __builtin_elementwise_max(v1[tn], z4));
-            const int ch = tn * 16 + q * 4;
-            *reinterpret_cast<half4*>(vw + crow_swz(wo, ch >> 3) + (ch & 7) * 2) = vv;
-          }
+          const half4 vv = __builtin_elementwise_max(__builtin_elementwise_max(prev[c][tn], v0),
+                                                     __builtin_elementwise_max(v1, z4));
+          const int ch = tn * 16 + q * 4;
+          *reinterpret_cast<half4*>(vw + crow_swz(wo, ch >> 3) + (ch & 7) * 2) = vv;
         }
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) prev[c][tn] = v1[tn];
+        prev[c][tn] = v1;
       };
-      conv_tile(0);
-      conv_tile(1);
-      epi_tile(0);
+      auto epi_tile = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) epi_tn(c, tn);
+      };
+      auto no_hook = [&](int) __attribute__((always_inline)) {};
+      conv_tile(0, no_hook);
+      if constexpr (IL) {
+        conv_tile(1, [&](int kh) __attribute__((always_inline)) {
+          if (kh >= 1 && kh <= TN) {
+            epi_tn(0, kh - 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        });
+      } else {
+        conv_tile(1, no_hook);
+        epi_tile(0);
+      }
       epi_tile(1);
       if (wid == 0) stamp(j);
       lds_barrier();
@@ -567,11 +589,11 @@ __global__ __launch_bounds__(512) void stem_role_fp16(const float* __restrict__ 
   }
 }
 
-template <int PBT, int D, bool PRE = false, int DBG = 0, bool XM = false>
+template <int PBT, int D, bool PRE = false, int DBG = 0, bool XM = false, bool BR = true, bool IL = true>
 static int run_stem4(const float* x, int B, int Cin, const _Float16* w, const float* bias, _Float16* out, hipStream_t s,
                      RgbdSrc src = RgbdSrc{}, unsigned long long* trace = nullptr) {
   PA_CHECK((size_t)B * 64 * 64 * 64 * 2 < 0x7fffffffu, "stem: output over 2 GB");
-  hipLaunchKernelGGL((stem_role_fp16<PBT, D, PRE, DBG, XM>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out,
+  hipLaunchKernelGGL((stem_role_fp16<PBT, D, PRE, DBG, XM, BR, IL>), dim3(64 / PBT, B), dim3(stem::NT), 0, s, x, B, Cin, w, bias, out,
                      src, trace);
   PA_LAUNCH_CHECK();
   return PA_OK;
@@ -628,6 +650,10 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     case 28: return run_stem4<4, 2>(x, B, Cin, w, bias, out, s);
     case 29: return run_stem4<32, 2>(x, B, Cin, w, bias, out, s);
     case 30: return run_stem4<16, 2, false, 0, true>(x, B, Cin, w, bias, out, s);  // XCD-grouped bands
+    case 31: return run_stem4<16, 2, false, 0, false, true, false>(x, B, Cin, w, bias, out, s);  // BR alone
+    case 32: return run_stem4<16, 2, false, 0, false, true, true>(x, B, Cin, w, bias, out, s);  // BR + IL
+    case 33: return run_stem4<16, 2, false, 0, false, false, true>(x, B, Cin, w, bias, out, s);  // IL
+    case 34: return run_stem4<16, 2, false, 0, false, false, false>(x, B, Cin, w, bias, out, s);  // neither (round 4)
     // shipped: version 4, the role split (29.3 vs 31.8 us per B = 64 launch, bit-identical;
     // prefetch depth 3 / 4 measured 29.7 / 30.4 us)
     default: break;

@@ -429,6 +429,9 @@ def test_kernel_variants_agree_bit_for_bit(B):
         (((1, 32),), y0),  # layer1: the one-tile patch kernel (independent of the shipped LDS-DMA kernel)
         (((7, 3),), y0),  # avgpool + fc fused into layer4's last conv instead of head_fp16
         (((0, 16),), y0),  # stem: version 3 (every wave convolves and moves rows) vs the shipped role split
+        (((0, 31),), y0),  # stem: bias as the first MFMA's accumulator input (BR) alone
+        (((0, 33),), y0),  # stem: IL alone
+        (((0, 34),), y0),  # stem: neither BR nor IL (round 4's form; shipped = both)
         (((1, 60),), y0),  # layer1: conv_c64d.hip (weights resident in LDS; shipped until round 5)
         (((1, 80),), y0),  # layer1: conv_c64v.hip 16-row tiles on every conv
         (((1, 81),), y0),  # layer1: conv_c64v.hip 8-row tiles, two 4-wave workgroups per CU, on every conv
