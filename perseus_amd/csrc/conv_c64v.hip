@@ -71,6 +71,8 @@ struct C64v {
 // arbitration on every SIMD runs ~30 % faster than its partner; with a static 4 tiles each the
 // launch ended ~3 us after the median workgroup (r05u trace), with stolen tiles it takes more.
 // The next tile's index is fetched one tile ahead (its patch is DMA'd during the current one).
+// Measured and not shipped: bit-identical but ~13 us slower per launch (2,048 device-scope
+// atomics on eight counters serialise, profiles/r05_c64v/r05ze_dyn_ab.log).
 template <int EPI, int TH, int DBG = 0, bool DYN = false>
 __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntiles) {
   using G = C64v<TH>;
@@ -78,8 +80,8 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   constexpr int PATCHB = G::PATCHB, PDW = G::PDW, RDW = G::RDW, BSTR = G::BSTR;
   constexpr bool RP = G::RP;
   constexpr int TM = 4, TN = 2;  // wave tile: 64 pixels (4 rows of 16) x 32 channels
-  // [patch 0 | patch 1 | residual tile]; the weights pass through [patch 1 | residual] in the
-  // prologue, before either is first written
+  // LDS layout: C64v::RP (the weights pass through the second half in the prologue, before it is
+  // first written)
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   char* patch = smem;
   auto resb = [&](int b) __attribute__((always_inline)) { return RP ? smem + b * BSTR + PATCHB : smem + 2 * PATCHB; };
@@ -372,8 +374,9 @@ static int run_c64v(const ConvArgs& a, hipStream_t s) {
 }
 
 // variant: 0 = 16-row tiles, one 8-wave workgroup per CU; 1 = 8-row tiles, two 4-wave
-// workgroups per CU; 4 / 6 = their s_memrealtime traces; 7 / 8 = timing only (wrong data): the
-// DMAs without their offset arithmetic
+// workgroups per CU; 2 (shipped, conv_patch.hip) = 16-row tiles on the plain convs, 8-row on the
+// residual ones; 3 / 5 = 1 / 2 with dynamic tiles (DYN); 4 / 6 = s_memrealtime traces; timing only
+// (wrong data): 7 / 8 = the DMAs without their offset arithmetic, 9 = every patch DMA on one tile
 int launch_conv3x3_c64v(const ConvArgs& a, int variant, hipStream_t s) {
   PA_CHECK(a.Cin == 64 && a.Cout == 64 && a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout,
            "c64v conv: Cin=Cout=64 stride-1 only");
