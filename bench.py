@@ -566,15 +566,19 @@ def factor_leg(dev, seed, rank, T=1000, L=24, reps=20):
 
 
 def csrc_digest() -> str:
-    """SHA-256 (16 hex) over the library's kernel sources and headers: the PMC record is
-    only valid for the exact kernels it was taken on."""
+    """SHA-256 (16 hex) over the library's kernel sources and headers with their comments
+    removed and whitespace runs collapsed: the PMC record is only valid for the exact kernels
+    it was taken on, and a comment-only edit does not change a kernel."""
     import glob
     import hashlib
+    import re
 
+    strip = re.compile(rb"//[^\n]*|/\*.*?\*/", re.S)
     h = hashlib.sha256()
     for f in sorted(glob.glob(os.path.join(ROOT, "perseus_amd", "csrc", "*"))):
         with open(f, "rb") as fh:
-            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+            code = b" ".join(strip.sub(b" ", fh.read()).split())
+        h.update(os.path.basename(f).encode() + b"\0" + code)
     return h.hexdigest()[:16]
 
 

@@ -58,3 +58,20 @@ def test_containers_and_factor_surface():
     p = smoother.KeypointProjectionFactor(0, nm, K, [1, 2], [0, 0, 0])
     assert p.pixel is None and p.keys() == [0]
 
+
+
+def test_csrc_digest_ignores_comments_not_code(tmp_path, monkeypatch):
+    """bench.csrc_digest keys the committed PMC records (profiles/pmc_*.json): a comment-only
+    edit of a kernel source keeps the record valid, a code edit invalidates it."""
+    import bench
+
+    src = tmp_path / "perseus_amd" / "csrc"
+    src.mkdir(parents=True)
+    f = src / "k.hip"
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    f.write_text("int a = 1;  // one\n/* block\n comment */ int b = 2;\n")
+    d0 = bench.csrc_digest()
+    f.write_text("// a new header line\nint a = 1;  // ONE\nint b = 2;   /* moved */\n")
+    assert bench.csrc_digest() == d0
+    f.write_text("int a = 1;\nint b = 3;\n")
+    assert bench.csrc_digest() != d0
