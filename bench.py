@@ -127,8 +127,7 @@ def main():
     model = KeypointCNN(num_channels=4, precision=args.precision)
     model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
     model.eval()
-    if os.environ.get("PERSEUS_AMD_BENCH_VARIANTS"):  # A/B of kernel variants (tools/gpu_check.sh benchab)
-        model.set_variants(dict(tuple(int(t) for t in lv.split(":")) for lv in os.environ["PERSEUS_AMD_BENCH_VARIANTS"].split(",")))
+    bench_variants(model)
     # this rank's frame shard, resident in HBM before timing
     x_host = synth.synthetic_frames(args.seed, B, first=rank * B)
     x = torch.from_numpy(x_host).to(dev)
@@ -234,6 +233,14 @@ def main():
     return line
 
 
+def bench_variants(m, env="PERSEUS_AMD_BENCH_VARIANTS"):
+    """A/B of kernel variants (tools/gpu_check.sh benchab / benchabx3): L:V[,L:V] from
+    PERSEUS_AMD_BENCH_VARIANTS on the headline model, from PERSEUS_AMD_BENCH_VARIANTS_PARITY on the
+    parity-mode models; unset in every recorded line."""
+    if os.environ.get(env):
+        m.set_variants(dict(tuple(int(t) for t in lv.split(":")) for lv in os.environ[env].split(",")))
+
+
 def parity_leg(state, x, yref, precision, B, dev, rank, warm=3, reps=20):
     """The parity-grade mode at the headline batch: frames/s over `reps` back-to-back
     forwards between HIP events on the forward's stream, its end-to-end MFMA-roofline
@@ -246,6 +253,7 @@ def parity_leg(state, x, yref, precision, B, dev, rank, warm=3, reps=20):
     m = KeypointCNN(num_channels=4, precision=precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
     m.eval()
+    bench_variants(m, "PERSEUS_AMD_BENCH_VARIANTS_PARITY")
     m.reserve(B, dev)
     out = torch.empty((B, 16), dtype=torch.float32, device=dev)
     for _ in range(warm):

@@ -140,6 +140,7 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
 int launch_stem_pool_x3(const float* x, int B, int Cin, const _Float16* w, const float* bias_s, const float* scale,
                         _Float16* out, hipStream_t s);
 int launch_conv3x3_x3_l1(const ConvArgs& a, hipStream_t s);
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s);
 int launch_conv3x3_x3_l2(const ConvArgs& a, hipStream_t s);
 int launch_conv3x3_x3_l3(const ConvArgs& a, hipStream_t s);
 int launch_conv3x3_x3_l4(const ConvArgs& a, hipStream_t s);

@@ -9,7 +9,11 @@ int launch_conv3x3_x3_l1(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(a.Hout == 64 && a.Wout == 64, "x3 conv layer1: %dx%d", a.Hout, a.Wout);
   // merged x_hi steps (conv_gx.h XM) shipped; variant 70 keeps three virtual blocks per 64 channels
   if (g_variant[1] == 70) return run_gx<16, 16, 1, 64, 4, 2, 64, 3, 1, 0, 1, true, true>(a, true, s);
-  return run_gx<16, 16, 1, 64, 4, 2, 64, 3, 1, 0, 1, true, true, true>(a, true, s);
+  // shipped (round 5): conv_x3v.hip, weights hi / lo in VGPRs, persistent 8-row tiles, bit-identical to
+  // the merged-step gx form (variant 91): layer1 -2.2 to -3.9 us per launch, parity mode +0.7 % on the
+  // driver's command, 5 of 6 interleaved pairs (profiles/r05_x3v/)
+  if (g_variant[1] == 91) return run_gx<16, 16, 1, 64, 4, 2, 64, 3, 1, 0, 1, true, true, true>(a, true, s);
+  return launch_conv3x3_x3v(a, s);
 }
 
 }  // namespace pa

@@ -379,6 +379,22 @@ def test_split_k_reduce_forms_bit_identical(precision):
     assert torch.equal(y0, y1)
 
 
+@pytest.mark.parametrize("B", [1, 3, 64])
+def test_fp16x3_layer1_vgpr_weight_kernel_bit_identical(B):
+    """fp16x3 layer1 on conv_x3v.hip (shipped: weights hi / lo in VGPRs, persistent 8-row tiles)
+    sums its products in conv_gx X3's merged-step order (variant 1:91) and splits the same way:
+    bit-identical."""
+    m = model(0, precision="fp16x3")
+    x = torch.from_numpy(synth.synthetic_frames(5, B)).cuda()
+    y0 = m(x)
+    try:
+        m.set_variants({1: 91})
+        y1 = m(x)
+    finally:
+        m.set_variants({})
+    assert torch.equal(y0, y1)
+
+
 def test_fp16x3_merged_steps_match_three_block_form(gold):
     """fp16x3 3x3 s1 convs: the merged x_hi steps (shipped: x_hi w_hi and x_hi w_lo from one
     fragment read) against three virtual blocks per 64 channels (variant 70).  The f32

@@ -12,6 +12,7 @@
 #   fwdab:L:V[,..]  interleaved whole-forward A/B (tools/head_ab.py --ab L:V ...)
 #   benchab:L:V[,L:V] the driver's bench command, shipped and with the variants
 #                   (PERSEUS_AMD_BENCH_VARIANTS), alternated $BENCHAB_PAIRS times -> benchab.jsonl
+#   benchabx3:L:V   the same for the parity-mode models (PERSEUS_AMD_BENCH_VARIANTS_PARITY)
 #   soab:A.so[,B.so] interleaved A/B of other builds of the library against the in-tree one
 #                   (tools/so_ab.py: one process per build and round; PERSEUS_AMD_LIB_AB)
 #   profile         rocprofv3 --kernel-trace --stats of the bench command + kernel traces of plain
@@ -68,12 +69,13 @@ step() {
       local spec=${s#fwdab:}
       (cd $R && timeout -k 10 400 $PY tools/head_ab.py --ab ${spec//,/ } ${AB_ARGS}) >> $O/fwdab.log 2>&1
       local rc=$?; tail -4 $O/fwdab.log; return $rc ;;
-    benchab:*)
-      local vs=${s#benchab:}
+    benchab:*|benchabx3:*)
+      local vs=${s#benchab:}; local ev=PERSEUS_AMD_BENCH_VARIANTS
+      if [[ $s == benchabx3:* ]]; then vs=${s#benchabx3:}; ev=PERSEUS_AMD_BENCH_VARIANTS_PARITY; fi
       for k in $(seq ${BENCHAB_PAIRS:-2}); do
         (cd $R && timeout -k 10 400 $PY bench.py --gpus 1 --steps 20 --warmup 5 --no-streaming) 2>>$O/benchab.err | \
           sed 's/^/{"ab": "shipped", "line": /; s/$/}/' >> $O/benchab.jsonl || return 1
-        (cd $R && PERSEUS_AMD_BENCH_VARIANTS=$vs timeout -k 10 400 $PY bench.py --gpus 1 --steps 20 --warmup 5 \
+        (cd $R && env $ev=$vs timeout -k 10 400 $PY bench.py --gpus 1 --steps 20 --warmup 5 \
           --no-streaming) 2>>$O/benchab.err | sed "s/^/{\"ab\": \"$vs\", \"line\": /; s/\$/}/" >> $O/benchab.jsonl || return 1
         echo "pair $k done"
       done ;;
