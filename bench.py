@@ -127,7 +127,7 @@ def main():
     model = KeypointCNN(num_channels=4, precision=args.precision)
     model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
     model.eval()
-    bench_variants(model)
+    variants = {"headline": bench_variants(model)}
     # this rank's frame shard, resident in HBM before timing
     x_host = synth.synthetic_frames(args.seed, B, first=rank * B)
     x = torch.from_numpy(x_host).to(dev)
@@ -157,9 +157,9 @@ def main():
             v = [model.time_launch(x, idx, REPS) for _ in range(args.profile_passes)]
             per_launch.append((idx, v[0][0], statistics.median(ms for _, ms in v)))
         fac = factor_leg(dev, args.seed, rank) if not args.no_factors else None
-        par = None if args.no_parity else parity_leg(state, x, yref, args.parity_precision, B, dev, rank)
+        par = None if args.no_parity else parity_leg(state, x, yref, args.parity_precision, B, dev, rank, variants)
         par32 = None if (args.no_parity or args.parity_precision == "fp32") else \
-            parity_leg(state, x, yref, "fp32", B, dev, rank)
+            parity_leg(state, x, yref, "fp32", B, dev, rank, variants)
         tset = None if args.no_trajset else trajset_leg(model, x, args, dev, world, rank)
 
         # ---- the timed region: W warm-up forwards, then exactly K forwards
@@ -225,6 +225,10 @@ def main():
             "kernels_ms": {f"{i:02d}_{n}": round(ms, 4) for i, n, ms in per_launch},
             "per_kernel_roofline": per_kernel,
             "factors": fac,
+            # kernel variants set on the models of this line ({} everywhere = the shipped kernels), and
+            # whether the library was a measurement build with the timing-only (wrong-result) variants
+            "variants": variants,
+            "timing_variants_built": bool(_lib_timing_variants()),
         }
         print(json.dumps(line))
     if world > 1:
@@ -236,12 +240,22 @@ def main():
 def bench_variants(m, env="PERSEUS_AMD_BENCH_VARIANTS"):
     """A/B of kernel variants (tools/gpu_check.sh benchab / benchabx3): L:V[,L:V] from
     PERSEUS_AMD_BENCH_VARIANTS on the headline model, from PERSEUS_AMD_BENCH_VARIANTS_PARITY on the
-    parity-mode models; unset in every recorded line."""
+    parity-mode models; unset in every recorded line.  Returns the map applied ({} = shipped
+    kernels), which the output line carries under "variants"."""
+    v = {}
     if os.environ.get(env):
-        m.set_variants(dict(tuple(int(t) for t in lv.split(":")) for lv in os.environ[env].split(",")))
+        v = dict(tuple(int(t) for t in lv.split(":")) for lv in os.environ[env].split(","))
+        m.set_variants(v)
+    return {str(k): val for k, val in v.items()}
 
 
-def parity_leg(state, x, yref, precision, B, dev, rank, warm=3, reps=20):
+def _lib_timing_variants() -> int:
+    from perseus_amd import _lib
+
+    return _lib.lib().pa_debug_timing_variants_built()
+
+
+def parity_leg(state, x, yref, precision, B, dev, rank, variants=None, warm=3, reps=20):
     """The parity-grade mode at the headline batch: frames/s over `reps` back-to-back
     forwards between HIP events on the forward's stream, its end-to-end MFMA-roofline
     fraction, and its px-L2 against the CPU f32 reference (rank 0)."""
@@ -253,7 +267,9 @@ def parity_leg(state, x, yref, precision, B, dev, rank, warm=3, reps=20):
     m = KeypointCNN(num_channels=4, precision=precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in state.items()})
     m.eval()
-    bench_variants(m, "PERSEUS_AMD_BENCH_VARIANTS_PARITY")
+    applied = bench_variants(m, "PERSEUS_AMD_BENCH_VARIANTS_PARITY")
+    if variants is not None:
+        variants[precision] = applied
     m.reserve(B, dev)
     out = torch.empty((B, 16), dtype=torch.float32, device=dev)
     for _ in range(warm):
@@ -579,15 +595,33 @@ def csrc_digest() -> str:
     it was taken on, and a comment-only edit does not change a kernel."""
     import glob
     import hashlib
-    import re
 
-    strip = re.compile(rb"//[^\n]*|/\*.*?\*/", re.S)
     h = hashlib.sha256()
     for f in sorted(glob.glob(os.path.join(ROOT, "perseus_amd", "csrc", "*"))):
         with open(f, "rb") as fh:
-            code = b" ".join(strip.sub(b" ", fh.read()).split())
+            code = strip_comments(fh.read())
         h.update(os.path.basename(f).encode() + b"\0" + code)
     return h.hexdigest()[:16]
+
+
+def strip_comments(src: bytes) -> bytes:
+    """C/C++ source without its comments (string and character literals kept intact, so a
+    "//" inside one is code), horizontal whitespace runs collapsed per line and blank lines
+    dropped; line breaks stay (they end preprocessor directives)."""
+    import re
+
+    tok = re.compile(rb'"(?:\\.|[^"\\\n])*"|\'(?:\\.|[^\'\\\n])*\'|//[^\n]*|/\*.*?\*/', re.S)
+
+    def repl(m):  # a comment is one space (C's translation phase 3); a literal is itself
+        t = m.group(0)
+        return b" " if t.startswith((b"//", b"/*")) else t
+
+    out = []
+    for line in tok.sub(repl, src).split(b"\n"):
+        line = b" ".join(line.split())
+        if line:
+            out.append(line)
+    return b"\n".join(out)
 
 
 def pmc_traffic(precision, B, idxs, names):
@@ -632,15 +666,16 @@ def pmc_mfma(precision, B, names):
                         "2.4 GHz) (the latter comparable with conv3x3_mfma_frac)"}
 
 
-def px_reference(state, x_host, nframes=None):
+def px_reference(state, x_host, nframes=64):
     """CPU f32 reference outputs (oracle/resnet_ref.py, the reference's own CPU path
-    restated) of the bench frames: the whole benched batch by default (max /
-    mean over 64 frames x 8 keypoints; ~1 s of CPU at 16 threads), or the first `nframes`."""
+    restated) of the first min(B, `nframes`) bench frames (max / mean over 64
+    frames x 8 keypoints; ~1 s of CPU at 16 threads; capped so that a --batch 1024 run does
+    not hold a 4 GB f32 stem map on the host)."""
     import torch
 
     from oracle import resnet_ref as R
 
-    return R.run(state, x_host if nframes is None else x_host[:nframes], torch.float32)
+    return R.run(state, x_host[:nframes], torch.float32)
 
 
 def px_error(model, x, yref):

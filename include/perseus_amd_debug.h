@@ -17,6 +17,10 @@ extern "C" {
  * `variant` for layer 1..4 (stage), 0 (stem), 5-7 (stride-2 entry / head options);
  * 0 = the shipped choice. */
 int pa_detector_debug_set_variant(pa_detector* d, int layer, int variant);
+/* Variants that give wrong results by construction (timing experiments) exist only in a
+ * measurement build (PERSEUS_AMD_TIMING_VARIANTS=1 when building); the release library
+ * returns PA_EINVAL for their ids (checked before the handle).  1 in a measurement build. */
+int pa_debug_timing_variants_built(void);
 
 /* Timestamping kernel variants write s_memrealtime stamps (100 MHz) to
  * trace_dev + launch * 65536 + workgroup * 64 (launch = index in the forward, stem = 0);

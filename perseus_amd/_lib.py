@@ -54,6 +54,7 @@ _SIGS = {
                                           C.c_int, C.c_void_p, C.c_void_p]),
     "pa_detector_debug_set_variant": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "pa_detector_debug_set_trace": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "pa_debug_timing_variants_built": (C.c_int, []),
     "pa_preprocess_rgbd": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.c_float, C.c_float, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "pa_keypoints_postprocess": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -29,6 +29,11 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mllvm", "-disable-promote-alloca-to-lds
          "-Wno-unused-variable", "-Wno-unused-result"]
 
 
+# measurement build: the timing-only kernel variants (wrong results by construction) compiled in
+# (csrc/common.h PA_TIMING_VARIANTS); the release library refuses their ids
+if os.environ.get("PERSEUS_AMD_TIMING_VARIANTS") == "1":
+    FLAGS.append("-DPA_TIMING_VARIANTS=1")
+
 OBJDIR = os.path.join(LIBDIR, "obj")  # incremental build state (git- and gpurun-ignored)
 # per-source extra hipcc flags (file name -> list); part of the flags digest
 EXTRA: dict = {}

@@ -8,6 +8,14 @@
 #include "../../include/perseus_amd.h"
 #include "../../include/perseus_amd_debug.h"
 
+// Timing-only kernel variants (wrong results by construction: MFMAs, DMAs, waits, stores or
+// offset arithmetic removed) exist only in a measurement build (PERSEUS_AMD_TIMING_VARIANTS=1 at
+// build time, perseus_amd/build.py -> -DPA_TIMING_VARIANTS=1).  The release library has no code
+// for them and pa_detector_debug_set_variant rejects their ids (detector.hip timing_only_variant).
+#ifndef PA_TIMING_VARIANTS
+#define PA_TIMING_VARIANTS 0
+#endif
+
 namespace pa {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));

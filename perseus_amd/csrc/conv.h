@@ -73,6 +73,9 @@ struct ConvS2Args {
   unsigned long long* trace;  // as ConvArgs::trace
   // split-K mode (conv_s2x.h PART): f32 partials [2][split][B][Hout][Wout][Cout] (conv, then downsample)
   float* part;
+  // conv_s2v.hip (the layer2 entry, 64 -> 128): conv + downsample weights in VGPR-fragment order
+  // (pa_detector build: [wave 4][fragment 20][tile 2][lane 64][8 fp16])
+  const void* wfrag;
 };
 
 template <typename T>
@@ -83,6 +86,8 @@ int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname);
 int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
 // fp16, 8 x 16 x 128 tiles with the row-split patch (conv_s2w.h), layers 2-3 (shipped there)
 int launch_conv3x3s2_w(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
+// fp16 layer2 entry (Cin 64 -> 128) with the weights in VGPRs (conv_s2v.hip; shipped from round 6)
+int launch_conv3x3s2_v(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
 
 template <typename T>
 int launch_conv(const ConvArgs& a, int ks, hipStream_t s, const char** kname);

@@ -269,9 +269,11 @@ int launch_conv3x3_c64(const ConvArgs& a, int variant, hipStream_t s) {
   switch (variant) {
     case 1: return run_c64<4>(a, s);
     case 5: return run_c64<8, 0, false>(a, s);  // plain (write-back) stores
-    case 7: return run_c64<8, 1>(a, s);
+#if PA_TIMING_VARIANTS
+    case 7: return run_c64<8, 1>(a, s);  // timing only (wrong results)
     case 8: return run_c64<8, 2>(a, s);
     case 9: return run_c64<8, 3>(a, s);
+#endif
     case 6: return a.trace ? run_c64<8, 4>(a, s) : run_c64<8>(a, s);
     default: return run_c64<8, 0, true>(a, s);
   }

@@ -198,11 +198,13 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   // straight into VGPRs had the waves of a channel half fetch the same bytes from L2: 295 KB per
   // workgroup, a 10 us prologue, r05q trace.)
   int j = blockIdx.x;
-  __shared__ int jnext_l;
+  // double-buffered by tile parity: tid 0 writes slot (t + 1) & 1 during tile t + 1 while a slow
+  // wave may still read slot t & 1 after tile t's hand-over barrier
+  __shared__ int jnext_l[2];
   const int x8 = blockIdx.x & 7;
   auto jof = [&](unsigned k) __attribute__((always_inline)) { return (int)gridDim.x + 8 * (int)k + x8; };
   if constexpr (DYN) {
-    if (tid == 0) jnext_l = jof(atomicAdd(a.cnt + x8, 1u));  // read after the prologue's barriers
+    if (tid == 0) jnext_l[1] = jof(atomicAdd(a.cnt + x8, 1u));  // read after the prologue's barriers
   }
   {
     const Org o0 = origin(tmap(j), true);
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   if constexpr (DBG == 4) trace_stamp(a.trace, 1);
 
   int jn = DYN ? 0 : j + (int)gridDim.x;
-  if constexpr (DYN) jn = __builtin_amdgcn_readfirstlane(jnext_l);
+  if constexpr (DYN) jn = __builtin_amdgcn_readfirstlane(jnext_l[1]);
   unsigned kdyn = 0;
   for (int t = 0; j < ntiles; ++t) {
     const int buf = t & 1;
@@ -307,7 +309,7 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
     });
     xwait_vm<0>();  // next patch (+ residual, + the dynamic fetch)
     if constexpr (DYN) {
-      if (tid == 0) jnext_l = has_next ? jof(kdyn) : ntiles;  // read after the hand-over barrier
+      if (tid == 0) jnext_l[t & 1] = has_next ? jof(kdyn) : ntiles;  // read after the hand-over barrier
     }
     if constexpr (DBG == 4) {  // (after the wait: a stamp's store would otherwise be waited for)
       trace_stamp(a.trace, 3 + 4 * t);
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
     if constexpr (DBG == 4) trace_stamp(a.trace, 5 + 4 * t);
     j = jn;
     if constexpr (DYN) {
-      jn = __builtin_amdgcn_readfirstlane(jnext_l);
+      jn = __builtin_amdgcn_readfirstlane(jnext_l[t & 1]);
     } else {
       jn = j + (int)gridDim.x;
     }
@@ -365,6 +367,11 @@ static int run_c64v(const ConvArgs& a, hipStream_t s) {
   const int tiles = a.B * (a.Hout / TH) * (a.Wout / 16);
   const int slots = conv_stream_cus(s) * (TH == 16 ? 1 : 2);  // resident workgroups
   const int grid = tiles < slots ? tiles : slots;
+  // dynamic tiles: workgroup b claims gridDim.x + 8 k + b % 8, which covers every tile only when
+  // all eight residues have a workgroup (a CU-masked stream of 1-3 CUs has fewer): static tiles
+  if constexpr (DYN) {
+    if (grid < 8) return run_c64v<TH, DBG, false>(a, s);
+  }
   if (a.epi & EPI_RES)
     hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES, TH, DBG, DYN>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
   else
@@ -390,9 +397,11 @@ int launch_conv3x3_c64v(const ConvArgs& a, int variant, hipStream_t s) {
   if (variant == 2) return (a.epi & EPI_RES) ? run_c64v<8, 0>(a, s) : run_c64v<16, 0>(a, s);
   if (variant == 3) return run_c64v<8, 0, true>(a, s);
   if (variant == 5) return (a.epi & EPI_RES) ? run_c64v<8, 0, true>(a, s) : run_c64v<16, 0>(a, s);
+#if PA_TIMING_VARIANTS
   if (variant == 7) return run_c64v<16, 7>(a, s);  // timing only: DMA offsets without arithmetic
   if (variant == 8) return run_c64v<8, 7>(a, s);
   if (variant == 9) return run_c64v<16, 8>(a, s);  // timing only: every patch DMA reads tile 1's patch
+#endif
   return run_c64v<16, 0>(a, s);
 }
 

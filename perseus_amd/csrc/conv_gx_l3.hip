@@ -10,13 +10,15 @@ int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s) {
   const bool xg = variant >= 10 || !(variant & 4);
   if (variant == 6) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 0, 1, false>(a, true, s);  // plain (write-back) stores
   if (variant == 7 && a.trace) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 4>(a, true, s);  // timestamps
-  if (variant == 8) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 2>(a, xg, s);  // timing only
-  if (variant == 9) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 3>(a, xg, s);  // timing only
-  // timing only (wrong results): 10 = DMAs, no waits / barriers; 11 = DMAs + barriers, no
-  // vmcnt waits; 12 = barriers only, no DMAs in the K loop
+#if PA_TIMING_VARIANTS
+  // timing only (wrong results): 8 = no DMAs in the K loop, 9 = no K loop, 10 = DMAs, no waits /
+  // barriers; 11 = DMAs + barriers, no vmcnt waits; 12 = barriers only, no DMAs in the K loop
+  if (variant == 8) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 2>(a, xg, s);
+  if (variant == 9) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 3>(a, xg, s);
   if (variant == 10) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 1>(a, xg, s);
   if (variant == 11) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 5>(a, xg, s);
   if (variant == 12) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 6>(a, xg, s);
+#endif
   switch (variant & 3) {
       case 1: return run_gx<8, 16, 1, 64, 2, 2, 256, 3>(a, xg, s);  // 80 KB LDS: 2 workgroups per CU
       case 2: return run_gx<16, 16, 1, 64, 4, 2, 256, 4, 3>(a, xg, s);

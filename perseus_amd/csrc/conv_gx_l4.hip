@@ -13,12 +13,14 @@ int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s) {
   // round-1 sweep ("measured and not shipped"): G = 3, fragments a full
   // step ahead, write-back stores, 4-wave tiles and ring distance 6 were removed from
   // the build (each fully unrolled 72-step kernel costs minutes of compile time)
+#if PA_TIMING_VARIANTS
   // timing only (wrong results), as layer3's 8-12
   if (variant == 10) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 1>(a, xgv_of(xg), s);
   if (variant == 11) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 5>(a, xgv_of(xg), s);
   if (variant == 12) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 6>(a, xgv_of(xg), s);
   if (variant == 13) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 2>(a, xgv_of(xg), s);
   if (variant == 14) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 3>(a, xgv_of(xg), s);
+#endif
   if (variant == 8 || variant == 9)  // 2-D XCD split: 4 / 2 channel groups per XCD
     return run_gx<8, 8, 2, 64, 4, 2, 512, 4>(a, variant == 8 ? 4 : 2, s);
   // shipped: 4 channel groups per XCD (round 2: HBM traffic 31-35 MB vs 46-51 per launch with the 1-D order,

@@ -315,10 +315,21 @@ int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) 
     // shipped: conv_s2w (layers 2 / 3; g_variant[6] = 40..47 its alternatives 0..7) and
     // conv_s2x (layer4; g_variant[6] = 10..39 its alternatives 0..29 on every layer); 3: the
     // one-tile kernel below (bit-identical reference of conv_s2x for the variant test)
+    // shipped from round 6: layer2 on conv_s2v.hip (weights in VGPRs; 6:50 its 8-wave 4 x 16 form,
+    // 6:52 / 6:53 the two with deferred stores, 6:49 / 6:51 / 6:54 trace variants; layers 3 / 4 as
+    // shipped under all of them),
+    // layer3 on conv_s2w, layer4 on conv_s2x.  6:40 = conv_s2w on layers 2 and 3 (the round-5
+    // kernels, bit-identical to conv_s2v); 48: layers 2 / 3 as shipped, layer4's entry in the 2 x 4
+    // XCD split (conv_s2x_l.hip variant 16)
     const int v = g_variant[6];
-    const bool w = v == 0 || (v >= 40 && v <= 47);
-    if (w && a.Hout != 8) return launch_conv3x3s2_w(a, v == 0 ? 0 : v - 40, s, kname);
-    if (w || (v >= 10 && v <= 39)) return launch_conv3x3s2_x(a, v >= 10 && v <= 39 ? v - 10 : 0, s, kname);
+    if ((v == 0 || (v >= 48 && v <= 54)) && a.Cin == 64 && a.Cout == 128 && a.wfrag) {
+      static const int sv[7] = {0, 4, 1, 5, 2, 3, 6};  // 6:48 .. 6:54 -> conv_s2v.hip variant
+      return launch_conv3x3s2_v(a, v == 0 ? 0 : sv[v - 48], s, kname);
+    }
+    const bool w = v == 0 || (v >= 40 && v <= 54);
+    if (w && a.Hout != 8) return launch_conv3x3s2_w(a, v == 0 || v >= 48 ? 0 : v - 40, s, kname);
+    if (w || (v >= 10 && v <= 39))
+      return launch_conv3x3s2_x(a, v >= 10 && v <= 39 ? v - 10 : v == 48 ? 16 : 0, s, kname);
   }
   if (a.Hout == 32) {
     if (kname) *kname = "conv3x3s2ds_l2";

@@ -97,7 +97,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
 
   const int ntn = Cout / BN;
   int tn_idx, sp;  // sp: the workgroup's group of TPW consecutive spatial tiles
-  if (xg) {  // blocks b and b + 8 share an XCD: the N-tiles of one spatial tile there
+  if (xg == 2) {  // 2 x 4 XCD split: XCD residue x8 takes channel half x8 & 1 of image group x8 >> 1
+    // (each XCD's L2 then holds half the weights and a quarter of the images: weight + input
+    // fetch 10.5 + 16.8 MB at layer4 / B = 64 instead of 21 + 8.4)
+    const int b = blockIdx.x, x8 = b & 7, i = b >> 3, nh = ntn >> 1;
+    tn_idx = (x8 & 1) * nh + i % nh;
+    sp = (i / nh) * 4 + (x8 >> 1);
+  } else if (xg) {  // blocks b and b + 8 share an XCD: the N-tiles of one spatial tile there
     const int b = blockIdx.x, x8 = b & 7, i = b >> 3;
     tn_idx = i % ntn;
     sp = (i / ntn) * 8 + x8;
@@ -351,7 +357,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3s2_x(ConvS2Args a, int xg
 
 template <int TH, int TW, int BN, int WM, int WN, int CIN, int PD, int G = 1, bool WT = true, bool X3 = false,
           int DBG = 0, int TPW = 1>
-static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
+static int run_s2x(const ConvS2Args& a, int xg, hipStream_t s) {
   PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "s2x conv: output over 2 GB");
   PA_CHECK(!X3 || (a.scale && a.scale2), "s2x conv (fp16x3): scales required");
   PA_CHECK(a.Cin == CIN, "s2x conv: Cin %d != %d", a.Cin, CIN);
@@ -362,7 +368,8 @@ static int run_s2x(const ConvS2Args& a, bool xg, hipStream_t s) {
            (a.Hout / TH) * (a.Wout / TW), TPW);
   const int ntn = a.Cout / BN;
   const int nsp = a.B * (a.Hout / TH) * (a.Wout / TW) / TPW;  // groups of TPW tiles
-  const int x = xg && nsp % 8 == 0;
+  // xg 2 (the 2 x 4 split) needs an even channel-tile count and image groups of 4; else the 1-D order
+  const int x = (xg == 2 && ntn % 2 == 0 && nsp % 4 == 0) ? 2 : (xg && nsp % 8 == 0) ? 1 : 0;
   hipLaunchKernelGGL((conv3x3s2_x<TH, TW, BN, WM, WN, CIN, PD, G, WT, X3, DBG, TPW>), dim3(nsp * ntn),
                      dim3(WM * WN * 64), 0, s, a, x);
   PA_LAUNCH_CHECK();

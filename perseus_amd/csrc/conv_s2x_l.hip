@@ -41,6 +41,7 @@ int launch_conv3x3s2_x(const ConvS2Args& a, int variant, hipStream_t s, const ch
     if (kname) *kname = "conv3x3s2x_l4";
     if (variant & 8) return run_s2x<8, 8, 128, 2, 4, 256, 3, 1, false>(a, xg, s);  // plain (write-back) stores
     if (variant == 7 && a.trace) return run_s2x<8, 8, 128, 2, 4, 256, 3, 1, true, false, 4>(a, xg, s);  // timestamps
+    if (variant == 16) return run_s2x<8, 8, 128, 2, 4, 256, 3>(a, 2, s);  // 2 x 4 XCD split (channel halves x image groups)
     switch (variant & 3) {
       case 1: return run_s2x<8, 8, 128, 2, 4, 256, 2>(a, xg, s);
       case 2: return run_s2x<8, 8, 64, 2, 2, 256, 4>(a, xg, s);

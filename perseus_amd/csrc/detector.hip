@@ -46,6 +46,7 @@ struct pa_detector {
   _Float16* w16 = nullptr;
   float* w32 = nullptr;
   float* bias = nullptr;
+  _Float16* wv2 = nullptr;  // layer2 entry (conv 3x3 s2 + ds, 64 -> 128) in VGPR-fragment order (conv_s2v.hip)
   _Float16* w3 = nullptr;   // fp16x3: per conv [cout][taps][hi (cin) | lo (cin)] of w * 2^e (stem: hi plane, lo plane)
   float* scl = nullptr;     // fp16x3: 2^-e per output channel (indexed like bias)
   float* bstem3 = nullptr;  // fp16x3 stem: bias * 2^e (the stem's accumulator starts from it)
@@ -191,6 +192,34 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
   PA_HIP(hipMemcpy(d->bias, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice));
   PA_HIP(hipMemcpy(d->fcw, fw, (size_t)nout * 512 * sizeof(float), hipMemcpyHostToDevice));
   PA_HIP(hipMemcpy(d->fcb, fb, (size_t)nout * sizeof(float), hipMemcpyHostToDevice));
+  // the layer2 entry's conv + downsample weights in conv_s2v.hip's register order: for wave wn
+  // (channel quarter), fragment k (< 18: tap k / 2, 32-channel half k & 1; 18, 19: the downsample's
+  // halves), tile tn, lane (q, r16): 8 fp16 of channel xperm(32 wn + 16 tn + r16), input channels
+  // 32 h + 8 q .. + 7 -- each wave-instruction loads 1 KB contiguous straight into the VGPRs the
+  // MFMA reads (no LDS staging)
+  {
+    const Block& b2 = d->blocks.size() > 2 ? d->blocks[2] : d->blocks[0];
+    if (b2.ds >= 0 && d->convs[b2.conv1].cin == 64 && d->convs[b2.conv1].cout == 128) {
+      const ConvL& c = d->convs[b2.conv1];
+      const ConvL& cd = d->convs[b2.ds];
+      std::vector<_Float16> hv((size_t)4 * 20 * 2 * 64 * 8);
+      for (int wn = 0; wn < 4; ++wn)
+        for (int k = 0; k < 20; ++k)
+          for (int tn = 0; tn < 2; ++tn)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int e = 0; e < 8; ++e) {
+                const int q = lane >> 4, r16 = lane & 15;
+                const int rho = 32 * wn + 16 * tn + r16;
+                const int co = (rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);  // xperm
+                const int h = k & 1, ci = 32 * h + 8 * q + e;
+                const _Float16 v = k < 18 ? h16[c.w_off + (size_t)co * 576 + (size_t)(k >> 1) * 64 + ci]
+                                          : h16[cd.w_off + (size_t)co * 64 + ci];
+                hv[((((size_t)wn * 20 + k) * 2 + tn) * 64 + lane) * 8 + e] = v;
+              }
+      PA_HIP(hipMalloc(&d->wv2, hv.size() * sizeof(_Float16)));
+      PA_HIP(hipMemcpy(d->wv2, hv.data(), hv.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
+  }
   PA_HIP(hipMalloc(&d->w3, h3.size() * sizeof(_Float16)));
   PA_HIP(hipMalloc(&d->scl, hs.size() * sizeof(float)));
   PA_HIP(hipMalloc(&d->bstem3, hbs.size() * sizeof(float)));
@@ -387,6 +416,8 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       sa.bias = d->bias + c1.b_off;
       sa.wds = wts + cd.w_off;
       sa.bias2 = d->bias + cd.b_off;
+      if constexpr (std::is_same<T, _Float16>::value)
+        sa.wfrag = (c1.cin == 64 && c1.cout == 128) ? d->wv2 : nullptr;  // conv_s2v.hip
       sa.out = Tb;
       sa.out2 = D;
       sa.B = B;
@@ -756,6 +787,7 @@ void pa_detector_destroy(pa_detector* d) {
   hipFree(d->fcw);
   hipFree(d->fcb);
   hipFree(d->w3);
+  if (d->wv2) hipFree(d->wv2);
   hipFree(d->scl);
   hipFree(d->bstem3);
   if (d->ws) hipFree(d->ws);
@@ -881,9 +913,27 @@ int pa_detector_debug_set_trace(pa_detector* d, unsigned long long* trace_dev) {
   return PA_OK;
 }
 
+// Variant ids whose kernels give wrong results by construction (timing experiments: MFMAs,
+// DMAs, waits, stores or offset arithmetic removed).  Only a PA_TIMING_VARIANTS build has them;
+// the release library refuses the ids, so no public call can reach wrong keypoints.
+static bool timing_only_variant(int layer, int v) {
+  switch (layer) {
+    case 0: return v == 21 || v == 22 || v == 23 || v == 25 || v == 26;  // stem.hip
+    case 1: return (v >= 37 && v <= 39) || v == 65 || v == 66 || (v >= 87 && v <= 89);  // c64, c64d, c64v
+    case 3: return v >= 58 && v <= 62;  // conv_gx_l3.hip 8-12
+    case 4: return v >= 60 && v <= 64;  // conv_gx_l4.hip 10-14
+    default: return false;
+  }
+}
+
+int pa_debug_timing_variants_built(void) { return PA_TIMING_VARIANTS; }
+
 int pa_detector_debug_set_variant(pa_detector* d, int layer, int variant) {
-  PA_CHECK(d, "null detector");
   PA_CHECK(layer >= 0 && layer < 8 && variant >= 0, "layer %d variant %d", layer, variant);
+  PA_CHECK(PA_TIMING_VARIANTS || !timing_only_variant(layer, variant),
+           "variant %d:%d is timing-only (wrong results): not in the release library (build with "
+           "PERSEUS_AMD_TIMING_VARIANTS=1)", layer, variant);
+  PA_CHECK(d, "null detector");
   d->variant[layer] = variant;
   return PA_OK;
 }

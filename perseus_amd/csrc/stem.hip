@@ -634,10 +634,12 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     case 12: return run_stem3<32, 3, true>(x, B, Cin, w, bias, out, s);
     case 15: return run_stem3<32, 2, true>(x, B, Cin, w, bias, out, s);
     case 13: return run_stem3<16, 2, false>(x, B, Cin, w, bias, out, s);  // plain (write-back) stores
+#if PA_TIMING_VARIANTS
     case 21: return run_stem3<16, 2, true, 1>(x, B, Cin, w, bias, out, s);  // timing only: no MFMAs
     case 22: return run_stem3<16, 2, true, 2>(x, B, Cin, w, bias, out, s);  // timing only: no pooling
     case 23: return run_stem3<16, 2, true, 3>(x, B, Cin, w, bias, out, s);  // timing only: no input rows
     case 25: return run_stem3<16, 2, true, 5>(x, B, Cin, w, bias, out, s);  // timing only: no conv-row writes
+#endif
     case 14:
       if (g_trace) return run_stem3<16, 2, true, 4>(x, B, Cin, w, bias, out, s, g_trace);  // timestamps
       break;
@@ -645,7 +647,9 @@ int launch_stem_pool_fp16(const float* x, int B, int Cin, const _Float16* w, con
     case 24:
       if (g_trace) return run_stem4<16, 2, false, 4>(x, B, Cin, w, bias, out, s, RgbdSrc{}, g_trace);  // timestamps
       break;
+#if PA_TIMING_VARIANTS
     case 26: return run_stem4<16, 2, false, 5>(x, B, Cin, w, bias, out, s);  // timing only: idle movers
+#endif
     case 27: return run_stem4<8, 2>(x, B, Cin, w, bias, out, s);  // shorter bands at any batch (A/B)
     case 28: return run_stem4<4, 2>(x, B, Cin, w, bias, out, s);
     case 29: return run_stem4<32, 2>(x, B, Cin, w, bias, out, s);

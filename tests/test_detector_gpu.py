@@ -21,7 +21,14 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 PX = 127.5
 FP32_PX_MAX = 1e-3
-FP16_PX_MAX = 0.1  # ~2x the observed 0.047 px max; fp16 activations over 20 layers
+# fp16 mode (the headline path) is not a parity mode: a regression bound near what it delivers
+# (max observed 0.0848 px on the golden case synthetic_b3_seed7, 0.0548 px over the bench's 64
+# frames x 8 keypoints, BENCH_r05; fp16 activations and weights over 20 layers), not the
+# north_star's 1e-3 px (was 0.1)
+FP16_PX_MAX = 0.09
+# fp16 integer pixels (streaming.py:143-144) on the bench batch: mismatches among coordinates
+# > 1e-3 px from an integer boundary, at most what round 5 measured (12 of 1,023, BENCH_r05)
+FP16_SAFE_INT_MISMATCH_MAX = 12
 
 
 def model(seed=0, in_ch=4, precision="fp16"):
@@ -122,9 +129,12 @@ def test_integer_keypoints_batch64(precision):
     tol = FP32_PX_MAX if precision in PARITY_MODES else FP16_PX_MAX
     frac = np.abs(px_ref - np.round(px_ref))
     mism = int_gpu != int_ref
-    print(f"{precision}: {int(mism.sum())} / {mism.size} integer mismatches "
-          f"({int((frac <= tol).sum())} coordinates within {tol} px of a boundary)")
+    safe = frac > FP32_PX_MAX
+    print(f"{precision}: {int(mism.sum())} / {mism.size} integer mismatches, {int((mism & safe).sum())} of "
+          f"{int(safe.sum())} safe ({int((frac <= tol).sum())} coordinates within {tol} px of a boundary)")
     assert not (mism & (frac > tol)).any()
+    if precision == "fp16":
+        assert int((mism & safe).sum()) <= FP16_SAFE_INT_MISMATCH_MAX
 
 
 @pytest.mark.parametrize("precision", PARITY_MODES)
@@ -418,7 +428,8 @@ def test_fp16x3_merged_steps_match_three_block_form(gold):
 
 @pytest.mark.parametrize("B", [1, 3, 64])
 def test_kernel_variants_agree_bit_for_bit(B):
-    """The persistent kernels (layer1 weight-resident conv, stride-2 + downsample)
+    """The persistent kernels (layer1 weight-resident conv, stride-2 + downsample; round 6: the
+    layer2 entry with its weights in VGPRs, conv_s2v.hip, against conv_s2w.h, variant 6:40)
     and the one-tile-per-workgroup kernels they replace accumulate in the same order:
     identical outputs, at batches below and above one tile per CU.  (Stem variants 10
     and 16 are version 3 of the stem at two band heights.)  The shipped layer2 / layer3
@@ -453,6 +464,8 @@ def test_kernel_variants_agree_bit_for_bit(B):
         (((1, 81),), y0),  # layer1: conv_c64v.hip 8-row tiles, two 4-wave workgroups per CU, on every conv
         (((1, 83),), y0),  # layer1: conv_c64v.hip 8-row tiles, tiles after the first from per-XCD counters
         (((0, 30), (1, 69)), y0),  # stem bands in XCD-grouped order; conv_c64d tiles in the plain order (same arithmetic)
+        (((6, 40),), y0),  # conv_s2w on layers 2 and 3 (round 5's entries) vs conv_s2v (layer2, weights in VGPRs)
+        (((6, 48),), y0),  # layer4's entry in the 2 x 4 XCD split (same arithmetic, another block -> tile map)
         (((6, 41),), y0),  # conv_s2w: layer2 one tile per workgroup, layer3 prefetch distance 2
         (((6, 42),), y0),  # conv_s2w: layer2 prefetch distance 2
         (((6, 44),), y0),  # conv_s2w: XCD-aware order off

@@ -75,3 +75,30 @@ def test_csrc_digest_ignores_comments_not_code(tmp_path, monkeypatch):
     assert bench.csrc_digest() == d0
     f.write_text("int a = 1;\nint b = 3;\n")
     assert bench.csrc_digest() != d0
+    # line breaks end preprocessor directives: joining two lines is a code change
+    f.write_text("#define N 4\nint c = N;\n")
+    d1 = bench.csrc_digest()
+    f.write_text("#define N 4 int c = N;\n")
+    assert bench.csrc_digest() != d1
+    # a "//" inside a string literal is code, not a comment
+    f.write_text('const char* s = "a//b";\n')
+    d2 = bench.csrc_digest()
+    f.write_text('const char* s = "a//c";\n')
+    assert bench.csrc_digest() != d2
+
+
+def test_timing_only_variants_rejected_by_release_library():
+    """The wrong-result timing variants (csrc/common.h PA_TIMING_VARIANTS) are not in the release
+    library: pa_detector_debug_set_variant refuses their ids before it looks at the handle, so no
+    public call can select them.  Shipped-alternative ids pass that check and
+    then fail only on the NULL handle.  No GPU call is made."""
+    from perseus_amd import _lib
+
+    L = _lib.lib()
+    assert L.pa_debug_timing_variants_built() == 0
+    for layer, v in ((0, 26), (1, 87), (1, 89), (1, 66), (1, 38), (3, 60), (4, 64)):
+        assert L.pa_detector_debug_set_variant(None, layer, v) < 0
+        assert b"timing-only" in L.pa_last_error(), (layer, v)
+    for layer, v in ((0, 34), (1, 80), (1, 60), (3, 53), (4, 58), (6, 41)):
+        assert L.pa_detector_debug_set_variant(None, layer, v) < 0
+        assert b"null detector" in L.pa_last_error(), (layer, v)

@@ -72,3 +72,88 @@ def test_split_tick_matches_fused(L, nk):
         # from here on the split tick continues from the fused tick's state
         for i in (1, 2, 3):  # pose, vel, angvel of the window
             slin["_keep"][i].copy_(flin["_keep"][i])
+
+
+def _setup_rows(tr, t0, t1, L, nk):
+    """prepare_trajectories over trajectories t0 .. t1 - 1 of `tr` (one set of synthetic
+    windows sliced, so a small launch sees exactly the bytes a large one does)."""
+    dev = torch.device("cuda", 0)
+    T = t1 - t0
+    r = slice(t0 * L, t1 * L)
+    nvalid = torch.full((T,), L - 2, dtype=torch.int32, device=dev)
+    y = torch.as_tensor(tr["y"][r], device=dev)
+    a, lin = pipeline.prepare_trajectories(y, tr["poses"][r], tr["vels"][r], tr["angvels"][r], tr["corners"],
+                                           tr["K"], T=T, L=L, dt=1 / 30, proj_sigmas=[2.0, 2.0],
+                                           dyn_sigmas=[0.1] * 6, cv_sigmas=[0.5] * 3, nvalid=nvalid)
+    out = dict(delta=torch.zeros((T * L, 12), dtype=torch.float64, device=dev),
+               info=torch.zeros(T, dtype=torch.int32, device=dev),
+               newest=torch.zeros((T, 12), dtype=torch.float64, device=dev))
+    return a, lin, out
+
+
+def test_ticks_with_more_trajectories_than_cus():
+    """the tick entry points take any T (one workgroup per trajectory, no grid-level
+    sync).  At T = CUs + 1, over three ticks: the fused tick (pa_window_pose_tick) and the split
+    tick (pre + post) give the first and the last three trajectories exactly the bits the same
+    windows get in T = 3 launches (no trajectory depends on how many others run, or on which CU
+    round it lands in), and the fused tick agrees with the four separate launches (cyclic
+    reduction forced: pa_debug_gn_set_assemblers(64), the fused tick's GN form) on every
+    trajectory -- info equal, delta to f64 rounding.  (On these random windows the fused
+    tick's projection factors differ from pa_trajectory_linearize's in the last bits on a few
+    trajectories -- two kernels, two FMA contractions -- so delta is compared to 1e-10 of its
+    scale, not bit for bit; on the streaming windows the two are bit-identical,
+    tests/test_streaming_pose_gpu.py.)"""
+    from perseus_amd import _lib
+
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    T, L, nk = ncu + 1, 24, 8
+    tr = synth.synthetic_trajectories(31, T, L, n_kp=nk)
+    fa, flin, fout = _setup_rows(tr, 0, T, L, nk)
+    qa, qlin, qout = _setup_rows(tr, 0, T, L, nk)
+    sa, slin, sout = _setup_rows(tr, 0, T, L, nk)
+    fsubs = [(t0, _setup_rows(tr, t0, t0 + 3, L, nk)) for t0 in (0, T - 3)]
+    ssubs = [(t0, _setup_rows(tr, t0, t0 + 3, L, nk)) for t0 in (0, T - 3)]
+    keep = qlin["_keep"]
+    win = {"y": keep[0].view(T, L, 2 * nk), "pose": keep[1].view(T, L, 12), "vel": keep[2].view(T, L, 3),
+           "angvel": keep[3].view(T, L, 3)}
+    plan = pipeline.GNPlan(qlin, T=T, L=L, lam=1e-2)
+    plan.out["delta"], plan.out["info"] = qout["delta"], qout["info"]
+    ws = pipeline.window_pose_tick_workspace(T, L, torch.device("cuda", 0))
+    ws3 = pipeline.window_pose_tick_workspace(3, L, torch.device("cuda", 0))
+    rng = np.random.default_rng(5)
+    L_ = _lib.lib()
+    for k in range(3):
+        y_new = torch.as_tensor((tr["y"].reshape(T, L, -1)[:, -1] + 0.01 * rng.standard_normal((T, 2 * nk)))
+                                .astype(np.float32), device="cuda").contiguous()
+        pipeline.window_pose_tick(fa, y_new, lam=1e-2, **fout)
+        for t0, (a3, _, o3) in fsubs:
+            pipeline.window_pose_tick(a3, y_new[t0:t0 + 3].contiguous(), lam=1e-2, **o3)
+        _lib.check(L_.pa_debug_gn_set_assemblers(64), "force cyclic reduction")
+        try:
+            pipeline.window_advance(y_new, win, dt=1 / 30, nvalid=keep[10])
+            pipeline.launch(qa, torch.device("cuda", 0))
+            plan.launch()
+            pipeline.window_retract(win, qout["delta"], qout["info"], newest=qout["newest"])
+            torch.cuda.synchronize()
+        finally:
+            L_.pa_debug_gn_set_assemblers(0)
+        pipeline.window_pose_tick_pre(sa, ws, lam=1e-2)
+        pipeline.window_pose_tick_post(sa, y_new, ws, **sout)
+        for t0, (a3, _, o3) in ssubs:
+            pipeline.window_pose_tick_pre(a3, ws3, lam=1e-2)
+            pipeline.window_pose_tick_post(a3, y_new[t0:t0 + 3].contiguous(), ws3, **o3)
+        torch.cuda.synchronize()
+        for big, subs in ((fout, fsubs), (sout, ssubs)):
+            for t0, (_, _, o3) in subs:
+                assert torch.equal(big["delta"][t0 * L:(t0 + 3) * L], o3["delta"]), (k, t0)
+                assert torch.equal(big["info"][t0:t0 + 3], o3["info"]), (k, t0)
+                assert torch.equal(big["newest"][t0:t0 + 3], o3["newest"]), (k, t0)
+        assert torch.equal(fout["info"], qout["info"]), k
+        assert int((fout["info"] == 0).sum()) >= T // 2
+        ok = fout["info"] == 0  # (an unsolved trajectory's delta is NaN in both forms)
+        df, dq = fout["delta"].view(T, -1)[ok], qout["delta"].view(T, -1)[ok]
+        assert (df - dq).abs().max().item() <= 1e-10 * df.abs().max().item(), k
+        np.testing.assert_array_equal(sout["info"].cpu().numpy(), fout["info"].cpu().numpy())
+        # the four-launch window continues from the fused tick's (they drift by rounding)
+        for i in (1, 2, 3):
+            qlin["_keep"][i].copy_(flin["_keep"][i])
