@@ -308,6 +308,10 @@ static int run_s2(const ConvS2Args& a, hipStream_t s) {
   return PA_OK;
 }
 
+// fp16 layer3 / layer4 entries with the weights in VGPRs and K split over the waves by input block
+// (conv_s2k.hip)
+int launch_conv3x3s2_k(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
+
 template <typename T>
 int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
@@ -322,7 +326,11 @@ int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) 
     // kernels, bit-identical to conv_s2v); 48: layers 2 / 3 as shipped, layer4's entry in the 2 x 4
     // XCD split (conv_s2x_l.hip variant 16)
     const int v = g_variant[6];
-    if ((v == 0 || (v >= 48 && v <= 54)) && a.Cin == 64 && a.Cout == 128 && a.wfrag) {
+    // 6:55 / 6:56: layers 3 and 4 on conv_s2k.hip (weights in VGPRs, K split over the waves by
+    // input block; 56 with s_memrealtime stamps), layer2 as shipped
+    if ((v == 55 || v == 56) && a.Cin >= 128 && a.wfrag) return launch_conv3x3s2_k(a, v - 55, s, kname);
+    if ((v == 0 || (v >= 48 && v <= 56)) && a.Cin == 64 && a.Cout == 128 && a.wfrag) {
+      if (v >= 55) return launch_conv3x3s2_v(a, 0, s, kname);
       static const int sv[7] = {0, 4, 1, 5, 2, 3, 6};  // 6:48 .. 6:54 -> conv_s2v.hip variant
       return launch_conv3x3s2_v(a, v == 0 ? 0 : sv[v - 48], s, kname);
     }

@@ -47,6 +47,8 @@ struct pa_detector {
   float* w32 = nullptr;
   float* bias = nullptr;
   _Float16* wv2 = nullptr;  // layer2 entry (conv 3x3 s2 + ds, 64 -> 128) in VGPR-fragment order (conv_s2v.hip)
+  _Float16* wv3 = nullptr;  // layer3 / layer4 entries (128 -> 256, 256 -> 512) in conv_s2k.hip's order
+  _Float16* wv4 = nullptr;
   _Float16* w3 = nullptr;   // fp16x3: per conv [cout][taps][hi (cin) | lo (cin)] of w * 2^e (stem: hi plane, lo plane)
   float* scl = nullptr;     // fp16x3: 2^-e per output channel (indexed like bias)
   float* bstem3 = nullptr;  // fp16x3 stem: bias * 2^e (the stem's accumulator starts from it)
@@ -197,28 +199,42 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
   // halves), tile tn, lane (q, r16): 8 fp16 of channel xperm(32 wn + 16 tn + r16), input channels
   // 32 h + 8 q .. + 7 -- each wave-instruction loads 1 KB contiguous straight into the VGPRs the
   // MFMA reads (no LDS staging)
-  {
-    const Block& b2 = d->blocks.size() > 2 ? d->blocks[2] : d->blocks[0];
-    if (b2.ds >= 0 && d->convs[b2.conv1].cin == 64 && d->convs[b2.conv1].cout == 128) {
-      const ConvL& c = d->convs[b2.conv1];
-      const ConvL& cd = d->convs[b2.ds];
-      std::vector<_Float16> hv((size_t)4 * 20 * 2 * 64 * 8);
-      for (int wn = 0; wn < 4; ++wn)
-        for (int k = 0; k < 20; ++k)
-          for (int tn = 0; tn < 2; ++tn)
-            for (int lane = 0; lane < 64; ++lane)
-              for (int e = 0; e < 8; ++e) {
-                const int q = lane >> 4, r16 = lane & 15;
-                const int rho = 32 * wn + 16 * tn + r16;
-                const int co = (rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3);  // xperm
-                const int h = k & 1, ci = 32 * h + 8 * q + e;
-                const _Float16 v = k < 18 ? h16[c.w_off + (size_t)co * 576 + (size_t)(k >> 1) * 64 + ci]
-                                          : h16[cd.w_off + (size_t)co * 64 + ci];
-                hv[((((size_t)wn * 20 + k) * 2 + tn) * 64 + lane) * 8 + e] = v;
-              }
-      PA_HIP(hipMalloc(&d->wv2, hv.size() * sizeof(_Float16)));
-      PA_HIP(hipMemcpy(d->wv2, hv.data(), hv.size() * sizeof(_Float16), hipMemcpyHostToDevice));
-    }
+  // The layer3 / layer4 entries' in conv_s2k.hip's order (the same per wave, for its 64-channel
+  // input block wb and its workgroup's channel half h): [h][wb][wn][fragment 20][tn 2][lane 64][8]
+  // of channel 32 WN h + xperm(32 wn + 16 tn + r16), input channels 64 wb + 32 (k & 1) + 8 q + e.
+  auto pack_vgpr = [&](const Block& bk, int wnq, _Float16** dst) -> int {
+    const ConvL& c = d->convs[bk.conv1];
+    const ConvL& cd = d->convs[bk.ds];
+    const int nb = c.cin / 64, nh = c.cout / (32 * wnq);
+    std::vector<_Float16> hv((size_t)nh * nb * wnq * 20 * 2 * 64 * 8);
+    for (int hh = 0; hh < nh; ++hh)
+      for (int wb = 0; wb < nb; ++wb)
+        for (int wn = 0; wn < wnq; ++wn)
+          for (int k = 0; k < 20; ++k)
+            for (int tn = 0; tn < 2; ++tn)
+              for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                  const int q = lane >> 4, r16 = lane & 15;
+                  const int rho = 32 * wn + 16 * tn + r16;
+                  const int co = 32 * wnq * hh + ((rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) |
+                                                  (rho & 3));  // xperm
+                  const int ci = 64 * wb + 32 * (k & 1) + 8 * q + e;
+                  const _Float16 v = k < 18 ? h16[c.w_off + (size_t)co * 9 * c.cin + (size_t)(k >> 1) * c.cin + ci]
+                                            : h16[cd.w_off + (size_t)co * c.cin + ci];
+                  hv[((((((size_t)hh * nb + wb) * wnq + wn) * 20 + k) * 2 + tn) * 64 + lane) * 8 + e] = v;
+                }
+    PA_HIP(hipMalloc(dst, hv.size() * sizeof(_Float16)));
+    PA_HIP(hipMemcpy(*dst, hv.data(), hv.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    return PA_OK;
+  };
+  for (const Block& bk : d->blocks) {
+    if (bk.ds < 0) continue;
+    const ConvL& c = d->convs[bk.conv1];
+    int rc = PA_OK;
+    if (c.cin == 64 && c.cout == 128 && !d->wv2) rc = pack_vgpr(bk, 4, &d->wv2);
+    if (c.cin == 128 && c.cout == 256 && !d->wv3) rc = pack_vgpr(bk, 4, &d->wv3);
+    if (c.cin == 256 && c.cout == 512 && !d->wv4) rc = pack_vgpr(bk, 2, &d->wv4);
+    if (rc != PA_OK) return rc;
   }
   PA_HIP(hipMalloc(&d->w3, h3.size() * sizeof(_Float16)));
   PA_HIP(hipMalloc(&d->scl, hs.size() * sizeof(float)));
@@ -417,7 +433,10 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       sa.wds = wts + cd.w_off;
       sa.bias2 = d->bias + cd.b_off;
       if constexpr (std::is_same<T, _Float16>::value)
-        sa.wfrag = (c1.cin == 64 && c1.cout == 128) ? d->wv2 : nullptr;  // conv_s2v.hip
+        sa.wfrag = (c1.cin == 64 && c1.cout == 128)    ? d->wv2   // conv_s2v.hip
+                   : (c1.cin == 128 && c1.cout == 256) ? d->wv3   // conv_s2k.hip
+                   : (c1.cin == 256 && c1.cout == 512) ? d->wv4
+                                                       : nullptr;
       sa.out = Tb;
       sa.out2 = D;
       sa.B = B;
@@ -788,6 +807,8 @@ void pa_detector_destroy(pa_detector* d) {
   hipFree(d->fcb);
   hipFree(d->w3);
   if (d->wv2) hipFree(d->wv2);
+  if (d->wv3) hipFree(d->wv3);
+  if (d->wv4) hipFree(d->wv4);
   hipFree(d->scl);
   hipFree(d->bstem3);
   if (d->ws) hipFree(d->ws);

@@ -478,6 +478,34 @@ def test_kernel_variants_agree_bit_for_bit(B):
         assert torch.equal(run(vs), ref), vs
 
 
+@pytest.mark.parametrize("B", [1, 3, 64, 70])
+def test_s2k_entries_vgpr_weights_k_split(B):
+    """Layers 3 and 4's stride-2 entries on conv_s2k.hip (weights in VGPRs, the K sum split over
+    the waves by 64-channel input block and the partials added in block order; variant 6:55):
+    another f32 summation order than the LDS-ring kernels, so within 0.05 px of them (the bound
+    the two ring orders share, test_kernel_variants_agree_bit_for_bit); its timestamping form
+    (6:56) is bit-identical; deterministic over repeats; odd batches (70: a partial round of
+    tiles) included."""
+    m = model(0)
+    x = torch.from_numpy(synth.synthetic_frames(4, B)).cuda()
+    y0 = m(x)
+    buf = torch.zeros(24 * 65536, dtype=torch.int64, device="cuda")
+    try:
+        m.set_variants({6: 55})
+        y1 = m(x)
+        y1b = m(x)
+        m.set_variants({6: 56})
+        m.set_trace(buf)
+        y2 = m(x)
+    finally:
+        m.set_trace(None)
+        m.set_variants({})
+    assert (y0 - y1).abs().max().item() * PX <= 0.05
+    assert torch.equal(y1, y1b)
+    assert torch.equal(y1, y2)
+    assert int((buf != 0).sum().item()) > 0  # the stamps were written
+
+
 def test_forward_into_out_buffer():
     """forward(x, out=buf) writes the same keypoints into buf (bench.py's step) and rejects a bad buffer."""
     m = model(0)

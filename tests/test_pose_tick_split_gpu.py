@@ -152,7 +152,12 @@ def test_ticks_with_more_trajectories_than_cus():
         assert int((fout["info"] == 0).sum()) >= T // 2
         ok = fout["info"] == 0  # (an unsolved trajectory's delta is NaN in both forms)
         df, dq = fout["delta"].view(T, -1)[ok], qout["delta"].view(T, -1)[ok]
-        assert (df - dq).abs().max().item() <= 1e-10 * df.abs().max().item(), k
+        # tick 0 starts both chains from the same windows: delta to f64 rounding; later ticks start
+        # from windows that carry the last-bit differences of the two factor kernels through the
+        # retract, and these random windows' solves amplify them (measured 8.8e-8 of the scale at
+        # tick 1 on a T = 257 box, r06b): 1e-6 of the scale there
+        tol = 1e-10 if k == 0 else 1e-6
+        assert (df - dq).abs().max().item() <= tol * df.abs().max().item(), k
         np.testing.assert_array_equal(sout["info"].cpu().numpy(), fout["info"].cpu().numpy())
         # the four-launch window continues from the fused tick's (they drift by rounding)
         for i in (1, 2, 3):
