@@ -6,10 +6,18 @@
 
 namespace pa {
 
+// layer2's entry with the hi / lo weights in VGPRs (conv_x3s2v.hip)
+int launch_conv3x3s2_v3(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
+// layer3's with the hi / lo weights in VGPRs and K split over the waves by input block (conv_x3s2k.hip)
+int launch_conv3x3s2_k3(const ConvS2Args& a, int variant, hipStream_t s, const char** kname);
+
 int launch_conv3x3s2_x3(const ConvS2Args& a, hipStream_t s, const char** kname) {
   if (a.B <= 0) return PA_OK;
   const int v = g_variant[6];
   const bool s2x = v == 44 || v == 45;  // conv_s2x.h forms (A/B; 45 = its shipped tiles)
+  // 6:57 / 6:58: layer2 on conv_x3s2v.hip, layer3 on conv_x3s2k.hip (58: with s_memrealtime stamps)
+  if ((v == 57 || v == 58) && a.Hout == 32 && a.Cin == 64 && a.wfrag) return launch_conv3x3s2_v3(a, v - 57, s, kname);
+  if ((v == 57 || v == 58) && a.Hout == 16 && a.Cin == 128 && a.wfrag) return launch_conv3x3s2_k3(a, v - 57, s, kname);
   if (a.Hout == 32 && a.Cin == 64) {
     if (!s2x) {
       // 64-channel tiles (the 128-channel X3 tile spills 43-110 VGPRs), two per workgroup (variant 46: one):

@@ -49,6 +49,8 @@ struct pa_detector {
   _Float16* wv2 = nullptr;  // layer2 entry (conv 3x3 s2 + ds, 64 -> 128) in VGPR-fragment order (conv_s2v.hip)
   _Float16* wv3 = nullptr;  // layer3 / layer4 entries (128 -> 256, 256 -> 512) in conv_s2k.hip's order
   _Float16* wv4 = nullptr;
+  _Float16* wv2x3 = nullptr;  // fp16x3 layer2 entry's hi / lo planes in conv_x3s2v.hip's register order
+  _Float16* wv3x3 = nullptr;  // fp16x3 layer3 entry's in conv_x3s2k.hip's order
   _Float16* w3 = nullptr;   // fp16x3: per conv [cout][taps][hi (cin) | lo (cin)] of w * 2^e (stem: hi plane, lo plane)
   float* scl = nullptr;     // fp16x3: 2^-e per output channel (indexed like bias)
   float* bstem3 = nullptr;  // fp16x3 stem: bias * 2^e (the stem's accumulator starts from it)
@@ -235,6 +237,50 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
     if (c.cin == 128 && c.cout == 256 && !d->wv3) rc = pack_vgpr(bk, 4, &d->wv3);
     if (c.cin == 256 && c.cout == 512 && !d->wv4) rc = pack_vgpr(bk, 2, &d->wv4);
     if (rc != PA_OK) return rc;
+  }
+  // the fp16x3 layer2 entry's hi / lo planes in conv_x3s2v.hip's register order: [wave 8][fragment
+  // 20][plane 2][lane 64][8] of channel 16 wave + r16, input channels 32 (k & 1) + 8 q + e (fragment
+  // k < 18: tap k / 2; 18, 19: the downsample)
+  for (const Block& bk : d->blocks) {
+    const ConvL& c = d->convs[bk.conv1];
+    if (bk.ds < 0 || c.cin != 64 || c.cout != 128 || d->wv2x3) continue;
+    const ConvL& cd = d->convs[bk.ds];
+    std::vector<_Float16> hv((size_t)8 * 20 * 2 * 64 * 8);
+    for (int wn = 0; wn < 8; ++wn)
+      for (int k = 0; k < 20; ++k)
+        for (int pl = 0; pl < 2; ++pl)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int e = 0; e < 8; ++e) {
+              const int q = lane >> 4, r16 = lane & 15, co = 16 * wn + r16, ci = 32 * (k & 1) + 8 * q + e;
+              const _Float16 v = k < 18 ? h3[c.w3_off + ((size_t)co * 9 + (k >> 1)) * 128 + pl * 64 + ci]
+                                        : h3[cd.w3_off + (size_t)co * 128 + pl * 64 + ci];
+              hv[((((size_t)wn * 20 + k) * 2 + pl) * 64 + lane) * 8 + e] = v;
+            }
+    PA_HIP(hipMalloc(&d->wv2x3, hv.size() * sizeof(_Float16)));
+    PA_HIP(hipMemcpy(d->wv2x3, hv.data(), hv.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+  }
+  // the fp16x3 layer3 entry's in conv_x3s2k.hip's order: [quarter h][block wb][tile wc][fragment
+  // 20][plane 2][lane 64][8] of channel 64 h + 16 wc + r16, input channels 64 wb + 32 (k & 1) + 8 q + e
+  for (const Block& bk : d->blocks) {
+    const ConvL& c = d->convs[bk.conv1];
+    if (bk.ds < 0 || c.cin != 128 || c.cout != 256 || d->wv3x3) continue;
+    const ConvL& cd = d->convs[bk.ds];
+    std::vector<_Float16> hv((size_t)4 * 2 * 4 * 20 * 2 * 64 * 8);
+    for (int hh = 0; hh < 4; ++hh)
+      for (int wb = 0; wb < 2; ++wb)
+        for (int wc = 0; wc < 4; ++wc)
+          for (int k = 0; k < 20; ++k)
+            for (int pl = 0; pl < 2; ++pl)
+              for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                  const int q = lane >> 4, r16 = lane & 15, co = 64 * hh + 16 * wc + r16;
+                  const int ci = 64 * wb + 32 * (k & 1) + 8 * q + e;
+                  const _Float16 v = k < 18 ? h3[c.w3_off + ((size_t)co * 9 + (k >> 1)) * 256 + pl * 128 + ci]
+                                            : h3[cd.w3_off + (size_t)co * 256 + pl * 128 + ci];
+                  hv[((((((size_t)hh * 2 + wb) * 4 + wc) * 20 + k) * 2 + pl) * 64 + lane) * 8 + e] = v;
+                }
+    PA_HIP(hipMalloc(&d->wv3x3, hv.size() * sizeof(_Float16)));
+    PA_HIP(hipMemcpy(d->wv3x3, hv.data(), hv.size() * sizeof(_Float16), hipMemcpyHostToDevice));
   }
   PA_HIP(hipMalloc(&d->w3, h3.size() * sizeof(_Float16)));
   PA_HIP(hipMalloc(&d->scl, hs.size() * sizeof(float)));
@@ -611,6 +657,9 @@ static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream
       sa.wds = d->w3 + cd.w3_off;
       sa.bias2 = d->bias + cd.b_off;
       sa.scale2 = d->scl + cd.b_off;
+      sa.wfrag = (c1.cin == 64 && c1.cout == 128)    ? d->wv2x3  // conv_x3s2v.hip
+                 : (c1.cin == 128 && c1.cout == 256) ? d->wv3x3  // conv_x3s2k.hip
+                                                     : nullptr;
       sa.out = Tb;
       sa.out2 = D;
       sa.B = B;
@@ -809,6 +858,8 @@ void pa_detector_destroy(pa_detector* d) {
   if (d->wv2) hipFree(d->wv2);
   if (d->wv3) hipFree(d->wv3);
   if (d->wv4) hipFree(d->wv4);
+  if (d->wv2x3) hipFree(d->wv2x3);
+  if (d->wv3x3) hipFree(d->wv3x3);
   hipFree(d->scl);
   hipFree(d->bstem3);
   if (d->ws) hipFree(d->ws);

@@ -354,6 +354,40 @@ def test_fp16x3_stride2_variants_agree_bit_for_bit(gold):
         assert np.abs(y - gold[f"{name}/y_ref_f32"]).max() * PX <= FP32_PX_MAX
 
 
+@pytest.mark.parametrize("B", [1, 5, 64, 70])
+def test_fp16x3_entries_vgpr_weights(gold, B):
+    """fp16x3 layer2 / layer3 entries with the hi / lo weights in VGPRs (variant 6:57: layer2 on
+    conv_x3s2v.hip, layer3 on conv_x3s2k.hip, its K sum split over the waves by input block): the
+    products summed group by group (x_hi w_hi, x_hi w_lo, x_lo w_hi) instead of conv_s2w.h X3's
+    plane by plane, so within f32 rounding of the shipped kernels (1e-4 px, as the two stride-2
+    families above); the timestamping forms (6:58) bit-identical; deterministic; and at the golden
+    outputs' 1e-3 px (the reference's own CPU keypoints and the f64 oracle)."""
+    m = model(0, precision="fp16x3")
+    x = torch.from_numpy(synth.synthetic_frames(4, B)).cuda()
+    y0 = m(x)
+    buf = torch.zeros(24 * 65536, dtype=torch.int64, device="cuda")
+    try:
+        m.set_variants({6: 57})
+        y1, y1b = m(x), m(x)
+        m.set_variants({6: 58})
+        m.set_trace(buf)
+        y2 = m(x)
+    finally:
+        m.set_trace(None)
+        m.set_variants({})
+    assert (y0 - y1).abs().max().item() * PX <= 1e-4
+    assert torch.equal(y1, y1b) and torch.equal(y1, y2)
+    name, seed, xg = cases()[3]
+    mg = model(seed, precision="fp16x3")
+    try:
+        mg.set_variants({6: 57})
+        y = mg(torch.from_numpy(xg).cuda()).cpu().numpy()
+    finally:
+        mg.set_variants({})
+    assert np.abs(y - gold[f"{name}/y_ref_f32"]).max() * PX <= FP32_PX_MAX
+    assert np.abs(y - gold[f"{name}/y_oracle_f64"]).max() * PX <= FP32_PX_MAX
+
+
 @pytest.mark.parametrize("B,small", [(64, False), (5, False), (3, True)])
 def test_fp16x3_stem_role_split_is_bit_identical(B, small):
     """fp16x3 stem: the role-split kernel (shipped) against the all-waves form (variant 30):
