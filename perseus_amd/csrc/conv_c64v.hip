@@ -73,7 +73,13 @@ struct C64v {
 // The next tile's index is fetched one tile ahead (its patch is DMA'd during the current one).
 // Measured and not shipped: bit-identical but ~13 us slower per launch (2,048 device-scope
 // atomics on eight counters serialise, profiles/r05_c64v/r05ze_dyn_ab.log).
-template <int EPI, int TH, int DBG = 0, bool DYN = false>
+// DS (deferred stores, conv_s2v.hip's): a tile's outputs go out during the next tile's K loop, one
+// 16-byte store per group after its DMAs, instead of at the tile's end, where every CU issues its
+// stores at about the same moment and they queue behind the whole chip's (0.84 us per tile from K
+// loop done to stores issued on the 16-row form, profiles/r06e trace).  Plain convs (RP): the
+// outputs are staged in the idle residual buffer of the tile (the residual tile's layout: 4 VGPRs
+// per store, read back just before it); residual convs: held in 16 VGPRs (pend).
+template <int EPI, int TH, int DBG = 0, bool DYN = false, bool DS = false>
 __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntiles) {
   using G = C64v<TH>;
   constexpr int TW = G::TW, PW = G::PW, NP = G::NP, NWAVE = G::NWAVE, PXB = G::PXB, PJ = G::PJ;
@@ -250,6 +256,14 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   int jn = DYN ? 0 : j + (int)gridDim.x;
   if constexpr (DYN) jn = __builtin_amdgcn_readfirstlane(jnext_l[1]);
   unsigned kdyn = 0;
+  static_assert(!(DS && DYN), "deferred stores with static tiles");
+  _Float16* __restrict__ out = (_Float16*)a.out;
+  constexpr bool DSL = DS && RP && !(EPI & EPI_RES);  // DS through LDS (the residual buffers are idle)
+  half8 pend[DSL ? 1 : TM];  // DS in VGPRs: the previous tile's outputs, rows 4 wm + tm
+  unsigned pend_base = 0;  // DS: their tile's byte offset (wave-uniform)
+  // this lane's byte offset in a tile: row 4 wm (+ tm rows), column o, channels 32 wn + 8 q
+  const unsigned olane = (unsigned)(((wm * 4 * W + o) * 64 + wn * 32 + q * 8) * 2);
+  const unsigned orow = (unsigned)(W * 128);
   for (int t = 0; j < ntiles; ++t) {
     const int buf = t & 1;
     const int tile = tmap(j);
@@ -304,10 +318,32 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
           dma_res(K - PDW, img, th0, tw0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (DS && K >= PDW + ((EPI & EPI_RES) ? RDW : 0) && K < PDW + ((EPI & EPI_RES) ? RDW : 0) + TM) {
+        constexpr int I = K - PDW - ((EPI & EPI_RES) ? RDW : 0);  // the previous tile's row I (issued last)
+        __builtin_amdgcn_sched_barrier(0);
+        if (t > 0) {
+          if constexpr (DSL) {
+            const int px = (wm * 4 + I) * TW + o;  // staged in the previous tile's buffer
+            const half8 v = *reinterpret_cast<const half8*>(resb(buf ^ 1) + px * 128 + (((wn * 4 + q) ^ (px & 7)) << 4));
+            store16<true>(out, pend_base + olane + I * orow, v);
+          } else {
+            store16<true>(out, pend_base + olane + I * orow, pend[I]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
       mm(kc);
     });
-    xwait_vm<0>();  // next patch (+ residual, + the dynamic fetch)
+    // next patch (+ residual, + the dynamic fetch); DS: the previous tile's stores, issued after
+    // them, may stay in flight
+    if constexpr (DS) {
+      if (t > 0)
+        xwait_vm<TM>();
+      else
+        xwait_vm<0>();
+    } else {
+      xwait_vm<0>();
+    }
     if constexpr (DYN) {
       if (tid == 0) jnext_l[t & 1] = has_next ? jof(kdyn) : ntiles;  // read after the hand-over barrier
     }
@@ -317,7 +353,6 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
     }
     if constexpr (!RP && (EPI & EPI_RES)) lds_barrier();  // every wave's residual DMAs landed
 
-    _Float16* __restrict__ out = (_Float16*)a.out;
     f32x4 bias[TN];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) bias[tn] = *reinterpret_cast<const f32x4*>(bias_l + wn * 32 + q * 8 + tn * 4);
@@ -333,9 +368,16 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
         if constexpr (EPI & EPI_RES) v += (float)rv[e];
         hv[e] = (_Float16)fmaxf(v, 0.f);
       }
-      const unsigned ob = (unsigned)((((img * H + th0 + wm * 4 + tm) * W + tw0 + o) * 64 + wn * 32 + q * 8) * 2);
-      store16<true>(out, ob, hv);
+      if constexpr (DSL) {
+        *reinterpret_cast<half8*>(resb(buf) + px * 128 + (((wn * 4 + q) ^ (px & 7)) << 4)) = hv;
+      } else if constexpr (DS) {
+        pend[tm] = hv;
+      } else {
+        const unsigned ob = (unsigned)((((img * H + th0 + wm * 4 + tm) * W + tw0 + o) * 64 + wn * 32 + q * 8) * 2);
+        store16<true>(out, ob, hv);
+      }
     }
+    if constexpr (DS) pend_base = (unsigned)(((img * H + th0) * W + tw0) * 128);
     if constexpr (DBG == 4) trace_stamp(a.trace, 4 + 4 * t);
     // every wave's DMAs into buf ^ 1 landed (its wait above) and its reads of buf (and of the
     // residual tile) retired
@@ -346,6 +388,22 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
       jn = __builtin_amdgcn_readfirstlane(jnext_l[t & 1]);
     } else {
       jn = j + (int)gridDim.x;
+    }
+  }
+  if constexpr (DS) {  // the last tile's outputs
+    if ((int)blockIdx.x < ntiles) {
+      if constexpr (DSL) {  // (this wave's own staged writes: no barrier needed)
+        const int lb = (int)((((ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x) & 1));  // the last tile's buffer
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          const int px = (wm * 4 + tm) * TW + o;
+          const half8 v = *reinterpret_cast<const half8*>(resb(lb) + px * 128 + (((wn * 4 + q) ^ (px & 7)) << 4));
+          store16<true>(out, pend_base + olane + tm * orow, v);
+        }
+      } else {
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) store16<true>(out, pend_base + olane + tm * orow, pend[tm]);
+      }
     }
   }
   if constexpr (DYN) {  // the last workgroup out zeroes the counters (vector atomics)
@@ -360,7 +418,7 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   }
 }
 
-template <int TH, int DBG, bool DYN = false>
+template <int TH, int DBG, bool DYN = false, bool DS = false>
 static int run_c64v(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(!DYN || a.cnt, "c64v conv: dynamic tiles need the handle's counters");
   PA_CHECK(a.Hout % TH == 0 && a.Wout % 16 == 0, "c64v conv: %dx%d not tiled by %dx16", a.Hout, a.Wout, TH);
@@ -373,9 +431,9 @@ static int run_c64v(const ConvArgs& a, hipStream_t s) {
     if (grid < 8) return run_c64v<TH, DBG, false>(a, s);
   }
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES, TH, DBG, DYN>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES, TH, DBG, DYN, DS>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
   else
-    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU, TH, DBG, DYN>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU, TH, DBG, DYN, DS>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -397,6 +455,11 @@ int launch_conv3x3_c64v(const ConvArgs& a, int variant, hipStream_t s) {
   if (variant == 2) return (a.epi & EPI_RES) ? run_c64v<8, 0>(a, s) : run_c64v<16, 0>(a, s);
   if (variant == 3) return run_c64v<8, 0, true>(a, s);
   if (variant == 5) return (a.epi & EPI_RES) ? run_c64v<8, 0, true>(a, s) : run_c64v<16, 0>(a, s);
+  // 10: variant 2 with deferred stores (DS); 11 / 12: 16-row / 8-row DS with s_memrealtime stamps
+  if (variant == 10) return (a.epi & EPI_RES) ? run_c64v<8, 0, false, true>(a, s) : run_c64v<16, 0, false, true>(a, s);
+  if (variant == 13) return (a.epi & EPI_RES) ? run_c64v<8, 0>(a, s) : run_c64v<16, 0, false, true>(a, s);
+  if (variant == 11 && a.trace) return run_c64v<16, 4, false, true>(a, s);
+  if (variant == 12 && a.trace) return run_c64v<8, 4, false, true>(a, s);
 #if PA_TIMING_VARIANTS
   if (variant == 7) return run_c64v<16, 7>(a, s);  // timing only: DMA offsets without arithmetic
   if (variant == 8) return run_c64v<8, 7>(a, s);

@@ -332,7 +332,9 @@ int launch_conv3x3s2_ds(const ConvS2Args& a, hipStream_t s, const char** kname) 
     if ((v == 0 || (v >= 48 && v <= 56)) && a.Cin == 64 && a.Cout == 128 && a.wfrag) {
       if (v >= 55) return launch_conv3x3s2_v(a, 0, s, kname);
       static const int sv[7] = {0, 4, 1, 5, 2, 3, 6};  // 6:48 .. 6:54 -> conv_s2v.hip variant
-      return launch_conv3x3s2_v(a, v == 0 ? 0 : sv[v - 48], s, kname);
+      // shipped: variant 2, deferred stores (16.0 vs 16.8 us, profiles/r06e/ab.log); 6:48 keeps the
+      // stores at the tile end (variant 0)
+      return launch_conv3x3s2_v(a, v == 0 ? 2 : sv[v - 48], s, kname);
     }
     const bool w = v == 0 || (v >= 40 && v <= 54);
     if (w && a.Hout != 8) return launch_conv3x3s2_w(a, v == 0 || v >= 48 ? 0 : v - 40, s, kname);

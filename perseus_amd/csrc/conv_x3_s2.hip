@@ -17,7 +17,10 @@ int launch_conv3x3s2_x3(const ConvS2Args& a, hipStream_t s, const char** kname) 
   const bool s2x = v == 44 || v == 45;  // conv_s2x.h forms (A/B; 45 = its shipped tiles)
   // 6:57 / 6:58: layer2 on conv_x3s2v.hip, layer3 on conv_x3s2k.hip (58: with s_memrealtime stamps)
   if ((v == 57 || v == 58) && a.Hout == 32 && a.Cin == 64 && a.wfrag) return launch_conv3x3s2_v3(a, v - 57, s, kname);
-  if ((v == 57 || v == 58) && a.Hout == 16 && a.Cin == 128 && a.wfrag) return launch_conv3x3s2_k3(a, v - 57, s, kname);
+  // shipped from round 6: layer3 on conv_x3s2k.hip (35.9 vs 39.7 us, profiles/r06e/ab_x3.log); 6:59
+  // keeps round 5's conv_s2w.h X3 kernel there (and 6:46 / 44 / 45 below run their own forms)
+  if ((v == 0 || v == 57 || v == 58) && a.Hout == 16 && a.Cin == 128 && a.wfrag)
+    return launch_conv3x3s2_k3(a, v == 58 ? 1 : 0, s, kname);
   if (a.Hout == 32 && a.Cin == 64) {
     if (!s2x) {
       // 64-channel tiles (the 128-channel X3 tile spills 43-110 VGPRs), two per workgroup (variant 46: one):

@@ -154,7 +154,7 @@ def test_fp16x3_profile_and_precision_switch():
     prof, y = m.profile(x)
     names = [n for n, _ in prof]
     assert names[0] == "stem_x3_conv7x7_pool" and names[-1] == "avgpool_fc_x3" and len(names) == 18
-    assert names[5] == "conv3x3s2w3_l2" and names[9] == "conv3x3s2w3_l3" and names[1] == "conv3x3x3_l1"
+    assert names[5] == "conv3x3s2w3_l2" and names[9] == "conv3x3s2k3_l3" and names[1] == "conv3x3x3_l1"
     assert torch.equal(y, m(x))
     m.precision = "fp16"
     y16 = m(x)
@@ -325,10 +325,11 @@ def test_profile_reports_every_kernel():
 
 
 def test_fp16x3_stride2_variants_agree_bit_for_bit(gold):
-    """fp16x3 stride-2 entries: the shipped row-split kernel (conv_s2w.h X3) against its
-    one- / two-tile workgroup variant (same sum order: bit for bit); conv_s2x.h's 8-wave
-    tile (variant 45) against its 4-wave one (44), bit for bit; and the two kernel families
-    (taps summed in another order) within f32 rounding, both at the golden outputs' 1e-3 px."""
+    """fp16x3 stride-2 entries: the row-split kernel (conv_s2w.h X3; layer2 shipped, layer3 until
+    round 5: variant 59) against its one- / two-tile workgroup variant (same sum order: bit for
+    bit); conv_s2x.h's 8-wave tile (variant 45) against its 4-wave one (44), bit for bit; and the
+    kernel families (taps summed in other orders; shipped layer3 on conv_x3s2k.hip) within f32
+    rounding, at the golden outputs' 1e-3 px."""
     m = model(0, precision="fp16x3")
     x = torch.from_numpy(synth.synthetic_frames(4, 5)).cuda()
 
@@ -339,13 +340,14 @@ def test_fp16x3_stride2_variants_agree_bit_for_bit(gold):
         finally:
             m.set_variants({})
 
-    y0, y46, y45, y44 = m(x), run(46), run(45), run(44)
-    assert torch.equal(y0, y46)
+    y0, y59, y46, y45, y44 = m(x), run(59), run(46), run(45), run(44)
+    assert torch.equal(y59, y46)
     assert torch.equal(y45, y44)
     assert (y0 - y45).abs().max().item() * PX <= 1e-4
+    assert (y0 - y59).abs().max().item() * PX <= 1e-4
     name, seed, xg = cases()[0]
     mg = model(seed, precision="fp16x3")
-    for v in (0, 45):
+    for v in (0, 45, 59):
         try:
             mg.set_variants({6: v} if v else {})
             y = mg(torch.from_numpy(xg).cuda()).cpu().numpy()
@@ -497,9 +499,11 @@ def test_kernel_variants_agree_bit_for_bit(B):
         (((1, 80),), y0),  # layer1: conv_c64v.hip 16-row tiles on every conv
         (((1, 81),), y0),  # layer1: conv_c64v.hip 8-row tiles, two 4-wave workgroups per CU, on every conv
         (((1, 83),), y0),  # layer1: conv_c64v.hip 8-row tiles, tiles after the first from per-XCD counters
+        (((1, 93),), y0),  # layer1: conv_c64v.hip with deferred stores (plain: staged in LDS, residual: in VGPRs)
+        (((1, 96),), y0),  # layer1: deferred stores on the plain convs only
         (((0, 30), (1, 69)), y0),  # stem bands in XCD-grouped order; conv_c64d tiles in the plain order (same arithmetic)
         (((6, 40),), y0),  # conv_s2w on layers 2 and 3 (round 5's entries) vs conv_s2v (layer2, weights in VGPRs)
-        (((6, 48),), y0),  # layer4's entry in the 2 x 4 XCD split (same arithmetic, another block -> tile map)
+        (((6, 48),), y0),  # layer2's entry with its stores at the tile end (shipped: deferred); layer4's in the 2 x 4 XCD split
         (((6, 41),), y0),  # conv_s2w: layer2 one tile per workgroup, layer3 prefetch distance 2
         (((6, 42),), y0),  # conv_s2w: layer2 prefetch distance 2
         (((6, 44),), y0),  # conv_s2w: XCD-aware order off

@@ -20,6 +20,7 @@ def main():
     p.add_argument("--launch", type=int, nargs="+", required=True)
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--runs", type=int, default=5)
+    p.add_argument("--precision", default="fp16")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -28,7 +29,7 @@ def main():
     from perseus_amd.detector import KeypointCNN
 
     L = _lib.lib()
-    m = KeypointCNN(num_channels=4)
+    m = KeypointCNN(num_channels=4, precision=a.precision)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in synth.synthetic_state_dict(0).items()})
     x = torch.from_numpy(synth.synthetic_frames(0, a.batch)).cuda()
     buf = torch.zeros(24 * 65536, dtype=torch.int64, device="cuda")
