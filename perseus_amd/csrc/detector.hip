@@ -617,6 +617,8 @@ static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream
     PA_RUN(launch_stem_pool_x3(x, B, d->in_ch, d->w3 + st.w3_off, d->bstem3, d->scl + st.b_off, X, s),
            "stem_x3_conv7x7_pool");
   int hw = 64;
+  int launch = 1;  // stem = 0 (the trace slot of each launch, as forward_t)
+  auto trace = [&]() { return g_trace ? g_trace + (size_t)TRACE_LAUNCH * launch++ : nullptr; };
   for (const Block& b : d->blocks) {
     const ConvL& c1 = d->convs[b.conv1];
     const ConvL& c2 = d->convs[b.conv2];
@@ -670,6 +672,7 @@ static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream
       sa.Wout = ho;
       sa.Cout = c1.cout;
       sa.part = d->part;
+      sa.trace = trace();
       if (small)
         PA_RUN(launch_conv3x3s2_small_x3(sa, s, &kn), kn);
       else
@@ -685,6 +688,7 @@ static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream
       a.Cin = c1.cin;
       a.Cout = c1.cout;
       a.epi = EPI_RELU;
+      a.trace = trace();
       PA_RUN(s1(a), kn);
     }
     ConvArgs b2 = a;
@@ -699,6 +703,7 @@ static int forward_x3(pa_detector* d, const float* x, int B, float* y, hipStream
     b2.Cin = c2.cin;
     b2.Cout = c2.cout;
     b2.epi = EPI_RELU | EPI_RES;
+    b2.trace = trace();
     PA_RUN(s1(b2), kn);
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
