@@ -40,7 +40,8 @@ struct X3s2v {
   static constexpr int PJ = (NP * 17 + 63) / 64;        // patch wave-DMAs per tile (44)
   static constexpr int PDW = (PJ + NWAVE - 1) / NWAVE;  // per wave (6, the last round partial)
   static constexpr int PATCHB = PJ * 1024;
-  static constexpr int SMEM = 2 * PATCHB;
+  static constexpr int STG = 8 * 8 * 64 * 8;           // DS: a tile's outputs, 8 half4 per lane and wave
+  static constexpr int SMEM = 2 * PATCHB + STG;
   static_assert(SMEM + 512 * 4 <= 160 * 1024, "LDS");
 };
 
@@ -52,7 +53,11 @@ __device__ __forceinline__ void x3_store8(void* base, unsigned off, half4 v) {
 
 // DBG = 4: s_memrealtime stamps into a.trace (0 start, 1 first patch landed; tile t < 15: 2 + 4 t
 // start, 3 + 4 t K loop done and next patch landed, 4 + 4 t stores issued; 63 end)
-template <int DBG = 0>
+// DS (deferred stores): a tile's 8 output half4 per lane are staged in this wave's own 4 KB of LDS
+// and stored during the next tile's K loop (groups 6 .. 13, after the patch DMAs), instead of at
+// the tile's end, where every CU stores at the same moment (traced: ~1.5 us of store issue and
+// ~2.6 us of barrier per tile, profiles/r06g)
+template <int DBG = 0, bool DS = false>
 __global__ __launch_bounds__(512, 1) void conv3x3s2_v3(ConvS2Args a, int ntiles) {
   using G = X3s2v;
   constexpr int TW = G::TW, PW = G::PW, NP = G::NP, PXB = G::PXB, PJ = G::PJ, PDW = G::PDW, PATCHB = G::PATCHB;
@@ -151,6 +156,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3s2_v3(ConvS2Args a, int ntiles)
   _Float16* __restrict__ out = (_Float16*)a.out;
   _Float16* __restrict__ out2 = (_Float16*)a.out2;
   int jn = j + (int)gridDim.x;
+  // DS: this wave's staging slots (index s = tm * 4 + kind * 2 + plane), the lane's output offset
+  // within a tile (row tm adds tm * W * 512 bytes, lo plane + 256, out2 the same), the staged tile's base
+  char* stg = smem + 2 * PATCHB + wn * 8 * 512 + lane * 8;
+  const unsigned olane = (unsigned)((o * XS * Cout + 16 * wn + 4 * q) * 2);
+  unsigned pend_base = 0;
+  auto store_staged = [&](int sidx) __attribute__((always_inline)) {
+    const int tm = sidx >> 2, kind = (sidx >> 1) & 1, pl = sidx & 1;
+    const half4 v = *reinterpret_cast<const half4*>(stg + sidx * 512);
+    x3_store8(kind ? out2 : out, pend_base + olane + (unsigned)(tm * W * XS * Cout * 2 + pl * Cout * 2), v);
+  };
   // one tile; the first is its own copy of the body (FIRST): there the compiler's vmcnt waits hold
   // each group's MFMAs until that group's weight fragments have landed
   auto run_tile = [&](auto firstc, int t) __attribute__((always_inline)) {
@@ -214,10 +229,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3s2_v3(ConvS2Args a, int ntiles)
         __builtin_amdgcn_sched_barrier(0);
         dma_one(Gi, onext, buf ^ 1);  // (no next tile: onext.on = false, zeros into buf ^ 1)
         __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (DS && Gi < PDW + 8) {  // the previous tile's outputs
+        __builtin_amdgcn_sched_barrier(0);
+        if (t > 0) store_staged(Gi - PDW);
+        __builtin_amdgcn_sched_barrier(0);
       }
       mm(gc);
     });
-    xwait_vm<0>();  // next patch landed (this wave's DMAs)
+    // next patch landed (this wave's DMAs; DS: the previous tile's stores, issued after them, may
+    // stay in flight)
+    if constexpr (DS) {
+      if (t > 0)
+        xwait_vm<8>();
+      else
+        xwait_vm<0>();
+    } else {
+      xwait_vm<0>();
+    }
     if constexpr (DBG == 4) {
       if (t < 15) trace_stamp(a.trace, 3 + 4 * t);
     }
@@ -240,12 +268,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3s2_v3(ConvS2Args a, int ntiles)
         h2[e] = v2.hi;
         l2[e] = v2.lo;
       }
-      const unsigned ob = (unsigned)((((img * H + th0 + tm) * W + tw0 + o) * XS * Cout + ch) * 2);
-      x3_store8(out, ob, h1);
-      x3_store8(out, ob + Cout * 2, l1);
-      x3_store8(out2, ob, h2);
-      x3_store8(out2, ob + Cout * 2, l2);
+      if constexpr (DS) {
+        *reinterpret_cast<half4*>(stg + (tm * 4 + 0) * 512) = h1;
+        *reinterpret_cast<half4*>(stg + (tm * 4 + 1) * 512) = l1;
+        *reinterpret_cast<half4*>(stg + (tm * 4 + 2) * 512) = h2;
+        *reinterpret_cast<half4*>(stg + (tm * 4 + 3) * 512) = l2;
+      } else {
+        const unsigned ob = (unsigned)((((img * H + th0 + tm) * W + tw0 + o) * XS * Cout + ch) * 2);
+        x3_store8(out, ob, h1);
+        x3_store8(out, ob + Cout * 2, l1);
+        x3_store8(out2, ob, h2);
+        x3_store8(out2, ob + Cout * 2, l2);
+      }
     }
+    if constexpr (DS) pend_base = (unsigned)((((img * H + th0) * W + tw0) * XS * Cout) * 2);
     if constexpr (DBG == 4) {
       if (t < 15) trace_stamp(a.trace, 4 + 4 * t);
     }
@@ -257,13 +293,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3s2_v3(ConvS2Args a, int ntiles)
   const bool any = j < ntiles;
   if (any) run_tile(std::true_type{}, 0);
   for (int t = 1; j < ntiles; ++t) run_tile(std::false_type{}, t);  // (run_tile advances j)
+  if constexpr (DS) {  // the last tile's outputs (this wave's own staged writes)
+    if (any) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) store_staged(i);
+    }
+  }
   if constexpr (DBG == 4) {
     __builtin_amdgcn_s_waitcnt(0);
     trace_stamp(a.trace, 63);
   }
 }
 
-// variant 0: shipped form; 1: s_memrealtime stamps into a.trace
+// variant 0: stores at the tile end; 1: with s_memrealtime stamps into a.trace; 2 / 3: 0 / 1 with
+// deferred stores (DS)
 int launch_conv3x3s2_v3(const ConvS2Args& a, int variant, hipStream_t s, const char** kname) {
   PA_CHECK(a.wfrag, "x3 s2v conv: no VGPR-order weights (ConvS2Args::wfrag)");
   PA_CHECK(a.scale && a.scale2, "x3 s2v conv: scales required");
@@ -280,6 +323,10 @@ int launch_conv3x3s2_v3(const ConvS2Args& a, int variant, hipStream_t s, const c
   const int grid = tiles < slots ? tiles : slots;
   if (variant == 1 && a.trace)
     hipLaunchKernelGGL((conv3x3s2_v3<4>), dim3(grid), dim3(512), 0, s, a, tiles);
+  else if (variant == 2)
+    hipLaunchKernelGGL((conv3x3s2_v3<0, true>), dim3(grid), dim3(512), 0, s, a, tiles);
+  else if (variant == 3 && a.trace)
+    hipLaunchKernelGGL((conv3x3s2_v3<4, true>), dim3(grid), dim3(512), 0, s, a, tiles);
   else
     hipLaunchKernelGGL((conv3x3s2_v3<0>), dim3(grid), dim3(512), 0, s, a, tiles);
   PA_LAUNCH_CHECK();

@@ -154,7 +154,7 @@ def test_fp16x3_profile_and_precision_switch():
     prof, y = m.profile(x)
     names = [n for n, _ in prof]
     assert names[0] == "stem_x3_conv7x7_pool" and names[-1] == "avgpool_fc_x3" and len(names) == 18
-    assert names[5] == "conv3x3s2w3_l2" and names[9] == "conv3x3s2k3_l3" and names[1] == "conv3x3x3_l1"
+    assert names[5] == "conv3x3s2v3_l2" and names[9] == "conv3x3s2k3_l3" and names[1] == "conv3x3x3_l1"
     assert torch.equal(y, m(x))
     m.precision = "fp16"
     y16 = m(x)
@@ -325,11 +325,11 @@ def test_profile_reports_every_kernel():
 
 
 def test_fp16x3_stride2_variants_agree_bit_for_bit(gold):
-    """fp16x3 stride-2 entries: the row-split kernel (conv_s2w.h X3; layer2 shipped, layer3 until
-    round 5: variant 59) against its one- / two-tile workgroup variant (same sum order: bit for
-    bit); conv_s2x.h's 8-wave tile (variant 45) against its 4-wave one (44), bit for bit; and the
-    kernel families (taps summed in other orders; shipped layer3 on conv_x3s2k.hip) within f32
-    rounding, at the golden outputs' 1e-3 px."""
+    """fp16x3 stride-2 entries: the row-split kernel (conv_s2w.h X3; layers 2 and 3 until round 5:
+    variant 59) against its one- / two-tile workgroup variant (same sum order: bit for bit);
+    conv_s2x.h's 8-wave tile (variant 45) against its 4-wave one (44), bit for bit; and the kernel
+    families (taps summed in other orders; shipped: layer2 on conv_x3s2v.hip, layer3 on
+    conv_x3s2k.hip) within f32 rounding, at the golden outputs' 1e-3 px."""
     m = model(0, precision="fp16x3")
     x = torch.from_numpy(synth.synthetic_frames(4, 5)).cuda()
 
@@ -358,27 +358,32 @@ def test_fp16x3_stride2_variants_agree_bit_for_bit(gold):
 
 @pytest.mark.parametrize("B", [1, 5, 64, 70])
 def test_fp16x3_entries_vgpr_weights(gold, B):
-    """fp16x3 layer2 / layer3 entries with the hi / lo weights in VGPRs (variant 6:57: layer2 on
-    conv_x3s2v.hip, layer3 on conv_x3s2k.hip, its K sum split over the waves by input block): the
-    products summed group by group (x_hi w_hi, x_hi w_lo, x_lo w_hi) instead of conv_s2w.h X3's
-    plane by plane, so within f32 rounding of the shipped kernels (1e-4 px, as the two stride-2
-    families above); the timestamping forms (6:58) bit-identical; deterministic; and at the golden
-    outputs' 1e-3 px (the reference's own CPU keypoints and the f64 oracle)."""
+    """fp16x3 layer2 / layer3 entries with the hi / lo weights in VGPRs (shipped from round 6; 6:57
+    the same kernels: layer2 on conv_x3s2v.hip, layer3 on conv_x3s2k.hip, its K sum split over
+    the waves by input block): the products summed group by group (x_hi w_hi, x_hi w_lo, x_lo w_hi)
+    instead of conv_s2w.h X3's plane by plane, so within f32 rounding of round 5's kernels (6:59,
+    1e-4 px, as the two stride-2 families above); the timestamping (6:58) and deferred-store (6:60)
+    forms bit-identical; deterministic; and at the golden outputs' 1e-3 px (the reference's own CPU
+    keypoints and the f64 oracle)."""
     m = model(0, precision="fp16x3")
     x = torch.from_numpy(synth.synthetic_frames(4, B)).cuda()
     y0 = m(x)
     buf = torch.zeros(24 * 65536, dtype=torch.int64, device="cuda")
     try:
+        m.set_variants({6: 59})  # round 5's conv_s2w.h X3 entries
+        y5 = m(x)
         m.set_variants({6: 57})
         y1, y1b = m(x), m(x)
+        m.set_variants({6: 60})  # layer2 with deferred stores
+        y3 = m(x)
         m.set_variants({6: 58})
         m.set_trace(buf)
         y2 = m(x)
     finally:
         m.set_trace(None)
         m.set_variants({})
-    assert (y0 - y1).abs().max().item() * PX <= 1e-4
-    assert torch.equal(y1, y1b) and torch.equal(y1, y2)
+    assert (y5 - y1).abs().max().item() * PX <= 1e-4
+    assert torch.equal(y0, y1) and torch.equal(y1, y1b) and torch.equal(y1, y2) and torch.equal(y1, y3)
     name, seed, xg = cases()[3]
     mg = model(seed, precision="fp16x3")
     try:
