@@ -3,6 +3,10 @@
 #include "conv_gx.h"
 
 namespace pa {
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds);
+}
+
+namespace pa {
 
 int launch_conv3x3_x3_l1(const ConvArgs& a, hipStream_t s) {
   if (a.B <= 0) return PA_OK;
@@ -13,7 +17,8 @@ int launch_conv3x3_x3_l1(const ConvArgs& a, hipStream_t s) {
   // the merged-step gx form (variant 91): layer1 -2.2 to -3.9 us per launch, parity mode +0.7 % on the
   // driver's command, 5 of 6 interleaved pairs (profiles/r05_x3v/)
   if (g_variant[1] == 91) return run_gx<16, 16, 1, 64, 4, 2, 64, 3, 1, 0, 1, true, true, true>(a, true, s);
-  return launch_conv3x3_x3v(a, s);
+  // 1:92: conv_x3v.hip with deferred stores on the plain convs
+  return launch_conv3x3_x3v(a, s, g_variant[1] == 92);
 }
 
 }  // namespace pa

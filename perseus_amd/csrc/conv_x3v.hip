@@ -43,7 +43,10 @@ static_assert(2 * BSTR <= 160 * 1024, "LDS");
 // different bank quads
 __device__ __forceinline__ int x3v_wswz(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 
-template <int EPI>
+// DS (plain convs only: VGPRs): a tile's 8 output half4 stay in 16 VGPRs and are stored during the
+// next tile's K loop (steps 6 .. 13, after the patch DMAs) instead of at the tile's end
+// (conv_s2v.hip's deferred stores)
+template <int EPI, bool DS = false>
 __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
   using namespace x3v;
   constexpr int TM = 4;
@@ -152,6 +155,11 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
   stage(xic<0>{}, xic<WR0>{});
   stage(xic<WR0>{}, xic<9>{});
 
+  static_assert(!DS || !(EPI & EPI_RES), "deferred stores: plain convs");
+  _Float16* __restrict__ out = (_Float16*)a.out;
+  half4 ph[DS ? TM : 1], pl[DS ? TM : 1];  // DS: the previous tile's hi / lo outputs
+  int pend_base = 0;                        // DS: their tile's first element (wave-uniform)
+  const int olane = ((wm * 4) * W + o) * 128 + c0;
   for (int t = 0; j < ntiles; ++t, j += gridDim.x) {
     const int buf = t & 1;
     const int tile = tmap(j);
@@ -206,12 +214,25 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
         __builtin_amdgcn_sched_barrier(0);
         if (has_next) dma_res(K - PDW, onext.img, onext.h0 + 1, onext.x0 + 1, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (DS && K < PDW + 2 * TM) {  // the previous tile's outputs, row (K - PDW) / 2
+        constexpr int I = K - PDW;
+        __builtin_amdgcn_sched_barrier(0);
+        if (t > 0)
+          *reinterpret_cast<half4*>(out + pend_base + olane + (I >> 1) * W * 128 + (I & 1) * 64) = (I & 1) ? pl[I >> 1] : ph[I >> 1];
+        __builtin_amdgcn_sched_barrier(0);
       }
       mm(kc);
     });
-    xwait_vm<0>();  // next patch (+ next residual)
+    // next patch (+ next residual); DS: the previous tile's stores, issued after them, may stay in flight
+    if constexpr (DS) {
+      if (t > 0)
+        xwait_vm<2 * TM>();
+      else
+        xwait_vm<0>();
+    } else {
+      xwait_vm<0>();
+    }
 
-    _Float16* __restrict__ out = (_Float16*)a.out;
     const char* resl = smem + buf * BSTR + PATCHB;
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
@@ -232,15 +253,31 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
         hv[e] = hl.hi;
         lv[e] = hl.lo;
       }
-      const size_t pix = ((size_t)img * H + th0 + wm * 4 + tm) * W + tw0 + o;
-      *reinterpret_cast<half4*>(out + pix * 128 + c0) = hv;
-      *reinterpret_cast<half4*>(out + pix * 128 + 64 + c0) = lv;
+      if constexpr (DS) {
+        ph[tm] = hv;
+        pl[tm] = lv;
+      } else {
+        const size_t pix = ((size_t)img * H + th0 + wm * 4 + tm) * W + tw0 + o;
+        *reinterpret_cast<half4*>(out + pix * 128 + c0) = hv;
+        *reinterpret_cast<half4*>(out + pix * 128 + 64 + c0) = lv;
+      }
     }
+    if constexpr (DS) pend_base = ((img * H + th0) * W + tw0) * 128;
     lds_barrier();  // patch / residual buf ^ 1 landed everywhere; reads of buf retired
+  }
+  if constexpr (DS) {  // the last tile's outputs
+    if ((int)blockIdx.x < ntiles) {
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        *reinterpret_cast<half4*>(out + pend_base + olane + tm * W * 128) = ph[tm];
+        *reinterpret_cast<half4*>(out + pend_base + olane + tm * W * 128 + 64) = pl[tm];
+      }
+    }
   }
 }
 
-int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s) {
+// ds: the plain convs with deferred stores (DS)
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds) {
   PA_CHECK(a.Cin == 64 && a.Cout == 64 && a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout,
            "x3v conv: Cin=Cout=64 stride-1 only");
   PA_CHECK(a.Hout % x3v::TH == 0 && a.Wout % x3v::TW == 0 && a.Wout <= 96, "x3v conv: %dx%d", a.Hout, a.Wout);
@@ -253,10 +290,14 @@ int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s) {
   const int grid = tiles < cus ? tiles : cus;
   if (a.epi & EPI_RES)
     hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU | EPI_RES>), dim3(grid), dim3(512), 0, s, a, tiles);
+  else if (ds)
+    hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU, true>), dim3(grid), dim3(512), 0, s, a, tiles);
   else
     hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU>), dim3(grid), dim3(512), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
+
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s) { return launch_conv3x3_x3v(a, s, false); }
 
 }  // namespace pa

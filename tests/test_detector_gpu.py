@@ -434,16 +434,19 @@ def test_split_k_reduce_forms_bit_identical(precision):
 def test_fp16x3_layer1_vgpr_weight_kernel_bit_identical(B):
     """fp16x3 layer1 on conv_x3v.hip (shipped: weights hi / lo in VGPRs, persistent 8-row tiles)
     sums its products in conv_gx X3's merged-step order (variant 1:91) and splits the same way:
-    bit-identical."""
+    bit-identical; so is its deferred-store form on the plain convs (1:92)."""
     m = model(0, precision="fp16x3")
     x = torch.from_numpy(synth.synthetic_frames(5, B)).cuda()
     y0 = m(x)
     try:
         m.set_variants({1: 91})
         y1 = m(x)
+        m.set_variants({1: 92})
+        y2 = m(x)
     finally:
         m.set_variants({})
     assert torch.equal(y0, y1)
+    assert torch.equal(y0, y2)
 
 
 def test_fp16x3_merged_steps_match_three_block_form(gold):
