@@ -3,7 +3,7 @@
 #include "conv_gx.h"
 
 namespace pa {
-int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds);
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds, bool dsr);
 }
 
 namespace pa {
@@ -17,8 +17,11 @@ int launch_conv3x3_x3_l1(const ConvArgs& a, hipStream_t s) {
   // the merged-step gx form (variant 91): layer1 -2.2 to -3.9 us per launch, parity mode +0.7 % on the
   // driver's command, 5 of 6 interleaved pairs (profiles/r05_x3v/)
   if (g_variant[1] == 91) return run_gx<16, 16, 1, 64, 4, 2, 64, 3, 1, 0, 1, true, true, true>(a, true, s);
-  // 1:92: conv_x3v.hip with deferred stores on the plain convs
-  return launch_conv3x3_x3v(a, s, g_variant[1] == 92);
+  // round 6: the plain convs with deferred stores (53.3 vs 56.9 us per launch, profiles/r06j/ab.log;
+  // bit-identical); 1:90 keeps their stores at the tile end (1:92 = the shipped form); 1:98: the
+  // residual convs' stores deferred as well (staged in place of their residual)
+  const int v = g_variant[1];
+  return launch_conv3x3_x3v(a, s, v != 90, v == 98);
 }
 
 }  // namespace pa

@@ -24,8 +24,9 @@ int launch_conv3x3s2_x3(const ConvS2Args& a, hipStream_t s, const char** kname) 
   if ((v == 60 || v == 61) && a.Hout == 32 && a.Cin == 64 && a.wfrag) return launch_conv3x3s2_v3(a, v == 60 ? 2 : 3, s, kname);
   // shipped from round 6: layer3 on conv_x3s2k.hip (35.9 vs 39.7 us, profiles/r06e/ab_x3.log); 6:59
   // keeps round 5's conv_s2w.h X3 kernel on layers 2 and 3 (and 6:46 / 44 / 45 below run their own forms)
-  if ((v == 0 || (v >= 57 && v <= 61 && v != 59)) && a.Hout == 16 && a.Cin == 128 && a.wfrag)
-    return launch_conv3x3s2_k3(a, v == 58 ? 1 : 0, s, kname);
+  // 6:62: layer3's with deferred stores
+  if ((v == 0 || (v >= 57 && v <= 62 && v != 59)) && a.Hout == 16 && a.Cin == 128 && a.wfrag)
+    return launch_conv3x3s2_k3(a, v == 58 ? 1 : v == 62 ? 2 : 0, s, kname);
   if (a.Hout == 32 && a.Cin == 64) {
     if (!s2x) {
       // 64-channel tiles (the 128-channel X3 tile spills 43-110 VGPRs), two per workgroup (variant 46: one):

@@ -47,7 +47,9 @@ __device__ __forceinline__ void x3k_store8(void* base, unsigned off, half4 v) {
 
 // DBG = 4: s_memrealtime stamps into a.trace (0 start, 1 first patch landed; tile t < 20: 2 + 3 t
 // start, 3 + 3 t K loop done, 4 + 3 t hand-over barrier passed; 63 end)
-template <int DBG = 0>
+// DS: a tile's two output half4 per lane (its finalized group's hi and lo) are stored during the next
+// tile's K loop (the two groups after the patch DMAs) instead of at the tile's end
+template <int DBG = 0, bool DS = false>
 __global__ __launch_bounds__(512, 1) void conv3x3s2_k3(ConvS2Args a, int ntiles, int nh, int xo) {
   using G = X3s2k;
   constexpr int NB = G::NB, WC = G::WC, TW = G::TW, PW = G::PW, NP = G::NP, PXB = G::PXB, NRC = G::NRC;
@@ -162,6 +164,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3s2_k3(ConvS2Args a, int ntiles,
   _Float16* __restrict__ out = (_Float16*)a.out;
   _Float16* __restrict__ out2 = (_Float16*)a.out2;
   int jn = j + nslots;
+  half4 phi, plo;        // DS: the previous tile's outputs
+  unsigned pob = 0;      // DS: their byte offset (per lane)
+  _Float16* const dsto = wb ? out2 : out;
   auto run_tile = [&](auto firstc, int t) __attribute__((always_inline)) {
     const int buf = t & 1;
     const int tile = tmap(j);
@@ -206,6 +211,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3s2_k3(ConvS2Args a, int ntiles,
         __builtin_amdgcn_sched_barrier(0);
         dma_one(Gi, onext, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (DS && Gi < PDW + 2) {  // the previous tile's outputs
+        __builtin_amdgcn_sched_barrier(0);
+        if (t > 0) x3k_store8(dsto, Gi == PDW ? pob : pob + Cout * 2, Gi == PDW ? phi : plo);
+        __builtin_amdgcn_sched_barrier(0);
       }
       mm(gc);
     });
@@ -217,7 +226,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3s2_k3(ConvS2Args a, int ntiles,
     const f32x4 pc = (ahh + alh) + ahl, pd = (dhh + dlh) + dhl;
     char* xb = xch + buf * XB;
     *reinterpret_cast<f32x4*>(xb + ((wb * WC + wc) * 64 + lane) * 16) = wb ? pc : pd;
-    xwait_vm<0>();  // next patch landed (this wave's DMAs; the previous tile's stores)
+    // next patch landed (this wave's DMAs; DS: the previous tile's two stores, issued after them, may
+    // stay in flight)
+    if constexpr (DS) {
+      if (t > 0)
+        xwait_vm<2>();
+      else
+        xwait_vm<0>();
+    } else {
+      xwait_vm<0>();
+    }
     lds_barrier();  // every wave's, the partials written, every read of buf retired
     if constexpr (DBG == 4) {
       if (t < 20) trace_stamp(a.trace, 4 + 3 * t);
@@ -236,23 +254,34 @@ __global__ __launch_bounds__(512, 1) void conv3x3s2_k3(ConvS2Args a, int ntiles,
       hi[e] = s.hi;
       lo[e] = s.lo;
     }
-    _Float16* dst = wb ? out2 : out;
     const unsigned ob = (unsigned)((((img * H + y) * W + o) * XS * Cout + c0 + ch) * 2);
-    x3k_store8(dst, ob, hi);
-    x3k_store8(dst, ob + Cout * 2, lo);
+    if constexpr (DS) {
+      phi = hi;
+      plo = lo;
+      pob = ob;
+    } else {
+      x3k_store8(dsto, ob, hi);
+      x3k_store8(dsto, ob + Cout * 2, lo);
+    }
     j = jn;
     jn = j + nslots;
   };
   const bool any = j < ntiles;
   if (any) run_tile(std::true_type{}, 0);
   for (int t = 1; j < ntiles; ++t) run_tile(std::false_type{}, t);  // (run_tile advances j)
+  if constexpr (DS) {  // the last tile's outputs
+    if (any) {
+      x3k_store8(dsto, pob, phi);
+      x3k_store8(dsto, pob + Cout * 2, plo);
+    }
+  }
   if constexpr (DBG == 4) {
     __builtin_amdgcn_s_waitcnt(0);
     trace_stamp(a.trace, 63);
   }
 }
 
-// variant 0: shipped form; 1: s_memrealtime stamps into a.trace
+// variant 0: shipped form; 1: s_memrealtime stamps into a.trace; 2: deferred stores (DS)
 int launch_conv3x3s2_k3(const ConvS2Args& a, int variant, hipStream_t s, const char** kname) {
   PA_CHECK(a.wfrag, "x3 s2k conv: no VGPR-order weights (ConvS2Args::wfrag)");
   PA_CHECK(a.scale && a.scale2, "x3 s2k conv: scales required");
@@ -273,6 +302,8 @@ int launch_conv3x3s2_k3(const ConvS2Args& a, int variant, hipStream_t s, const c
   if (grid / nh > tiles) grid = (xo ? ((tiles + 7) / 8) * 8 : tiles) * nh;
   if (variant == 1 && a.trace)
     hipLaunchKernelGGL((conv3x3s2_k3<4>), dim3(grid), dim3(512), 0, s, a, tiles, nh, xo);
+  else if (variant == 2)
+    hipLaunchKernelGGL((conv3x3s2_k3<0, true>), dim3(grid), dim3(512), 0, s, a, tiles, nh, xo);
   else
     hipLaunchKernelGGL((conv3x3s2_k3<0>), dim3(grid), dim3(512), 0, s, a, tiles, nh, xo);
   PA_LAUNCH_CHECK();

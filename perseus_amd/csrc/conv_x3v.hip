@@ -43,9 +43,12 @@ static_assert(2 * BSTR <= 160 * 1024, "LDS");
 // different bank quads
 __device__ __forceinline__ int x3v_wswz(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 
-// DS (plain convs only: VGPRs): a tile's 8 output half4 stay in 16 VGPRs and are stored during the
-// next tile's K loop (steps 6 .. 13, after the patch DMAs) instead of at the tile's end
-// (conv_s2v.hip's deferred stores)
+// DS: a tile's 8 output half4 per lane are stored during the next tile's K loop (steps 6 .. 13, after
+// the patch DMAs) instead of at the tile's end (conv_s2v.hip's deferred stores).  Plain convs: held in
+// 16 VGPRs.  Residual convs (no VGPRs to spare): staged in place of the residual each lane has just
+// read (its own 8 + 8 bytes of the tile's residual buffer); that buffer receives the tile-after-next's
+// residual in the next K loop, so there the residual DMAs move behind the staged reads and an LDS
+// barrier (steps 14 .. 17).
 template <int EPI, bool DS = false>
 __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
   using namespace x3v;
@@ -155,9 +158,14 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
   stage(xic<0>{}, xic<WR0>{});
   stage(xic<WR0>{}, xic<9>{});
 
-  static_assert(!DS || !(EPI & EPI_RES), "deferred stores: plain convs");
+  constexpr bool DSR = DS && (EPI & EPI_RES);  // staged in the residual buffer
+  constexpr int RD0 = DSR ? PDW + 2 * TM : PDW;  // first residual-DMA step
   _Float16* __restrict__ out = (_Float16*)a.out;
-  half4 ph[DS ? TM : 1], pl[DS ? TM : 1];  // DS: the previous tile's hi / lo outputs
+  // DSR: this lane's staged chunk of tile pixel px, plane pl (the residual read's address)
+  auto stg_off = [&](int px, int pl) __attribute__((always_inline)) {
+    return px * 256 + (((8 * pl + (c0 >> 3)) ^ (px & 15)) << 4) + (c0 & 4) * 2;
+  };
+  half4 ph[DS && !DSR ? TM : 1], pl[DS && !DSR ? TM : 1];  // DS (plain): the previous tile's hi / lo outputs
   int pend_base = 0;                        // DS: their tile's first element (wave-uniform)
   const int olane = ((wm * 4) * W + o) * 128 + c0;
   for (int t = 0; j < ntiles; ++t, j += gridDim.x) {
@@ -210,21 +218,29 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
         __builtin_amdgcn_sched_barrier(0);
         dma_patch(K, onext, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr ((EPI & EPI_RES) && K < PDW + RDW) {  // the next tile's residual
+      } else if constexpr ((EPI & EPI_RES) && K >= RD0 && K < RD0 + RDW) {  // the next tile's residual
         __builtin_amdgcn_sched_barrier(0);
-        if (has_next) dma_res(K - PDW, onext.img, onext.h0 + 1, onext.x0 + 1, buf ^ 1);
+        if constexpr (DSR && K == RD0) lds_barrier();  // every wave's staged reads of buf ^ 1 retired
+        if (has_next) dma_res(K - RD0, onext.img, onext.h0 + 1, onext.x0 + 1, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (DS && K < PDW + 2 * TM) {  // the previous tile's outputs, row (K - PDW) / 2
+      } else if constexpr (DS && K >= PDW && K < PDW + 2 * TM) {  // the previous tile's outputs, row (K - PDW) / 2
         constexpr int I = K - PDW;
         __builtin_amdgcn_sched_barrier(0);
-        if (t > 0)
-          *reinterpret_cast<half4*>(out + pend_base + olane + (I >> 1) * W * 128 + (I & 1) * 64) = (I & 1) ? pl[I >> 1] : ph[I >> 1];
+        if (t > 0) {
+          half4 v;
+          if constexpr (DSR)
+            v = *reinterpret_cast<const half4*>(smem + (buf ^ 1) * BSTR + PATCHB + stg_off((wm * 4 + (I >> 1)) * TW + o, I & 1));
+          else
+            v = (I & 1) ? pl[I >> 1] : ph[I >> 1];
+          *reinterpret_cast<half4*>(out + pend_base + olane + (I >> 1) * W * 128 + (I & 1) * 64) = v;
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       mm(kc);
     });
-    // next patch (+ next residual); DS: the previous tile's stores, issued after them, may stay in flight
-    if constexpr (DS) {
+    // next patch (+ next residual); DS (plain): the previous tile's stores, issued after them, may stay
+    // in flight (DSR: the residual DMAs come after them)
+    if constexpr (DS && !DSR) {
       if (t > 0)
         xwait_vm<2 * TM>();
       else
@@ -253,7 +269,10 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
         hv[e] = hl.hi;
         lv[e] = hl.lo;
       }
-      if constexpr (DS) {
+      if constexpr (DSR) {  // in place of this lane's residual chunk
+        *reinterpret_cast<half4*>(smem + buf * BSTR + PATCHB + stg_off(px, 0)) = hv;
+        *reinterpret_cast<half4*>(smem + buf * BSTR + PATCHB + stg_off(px, 1)) = lv;
+      } else if constexpr (DS) {
         ph[tm] = hv;
         pl[tm] = lv;
       } else {
@@ -265,19 +284,28 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
     if constexpr (DS) pend_base = ((img * H + th0) * W + tw0) * 128;
     lds_barrier();  // patch / residual buf ^ 1 landed everywhere; reads of buf retired
   }
-  if constexpr (DS) {  // the last tile's outputs
+  if constexpr (DS) {  // the last tile's outputs (this lane's own staged chunks)
     if ((int)blockIdx.x < ntiles) {
+      const int lb = ((ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x) & 1;  // the last tile's buffer
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
-        *reinterpret_cast<half4*>(out + pend_base + olane + tm * W * 128) = ph[tm];
-        *reinterpret_cast<half4*>(out + pend_base + olane + tm * W * 128 + 64) = pl[tm];
+        half4 vh, vl;
+        if constexpr (DSR) {
+          vh = *reinterpret_cast<const half4*>(smem + lb * BSTR + PATCHB + stg_off((wm * 4 + tm) * TW + o, 0));
+          vl = *reinterpret_cast<const half4*>(smem + lb * BSTR + PATCHB + stg_off((wm * 4 + tm) * TW + o, 1));
+        } else {
+          vh = ph[tm];
+          vl = pl[tm];
+        }
+        *reinterpret_cast<half4*>(out + pend_base + olane + tm * W * 128) = vh;
+        *reinterpret_cast<half4*>(out + pend_base + olane + tm * W * 128 + 64) = vl;
       }
     }
   }
 }
 
-// ds: the plain convs with deferred stores (DS)
-int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds) {
+// ds / dsr: the plain / residual convs with deferred stores (DS)
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds, bool dsr) {
   PA_CHECK(a.Cin == 64 && a.Cout == 64 && a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout,
            "x3v conv: Cin=Cout=64 stride-1 only");
   PA_CHECK(a.Hout % x3v::TH == 0 && a.Wout % x3v::TW == 0 && a.Wout <= 96, "x3v conv: %dx%d", a.Hout, a.Wout);
@@ -288,7 +316,9 @@ int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds) {
   const int tiles = a.B * (a.Hout / x3v::TH) * (a.Wout / x3v::TW);
   const int cus = conv_stream_cus(s);
   const int grid = tiles < cus ? tiles : cus;
-  if (a.epi & EPI_RES)
+  if ((a.epi & EPI_RES) && dsr)
+    hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU | EPI_RES, true>), dim3(grid), dim3(512), 0, s, a, tiles);
+  else if (a.epi & EPI_RES)
     hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU | EPI_RES>), dim3(grid), dim3(512), 0, s, a, tiles);
   else if (ds)
     hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU, true>), dim3(grid), dim3(512), 0, s, a, tiles);
@@ -298,6 +328,6 @@ int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds) {
   return PA_OK;
 }
 
-int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s) { return launch_conv3x3_x3v(a, s, false); }
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s) { return launch_conv3x3_x3v(a, s, false, false); }
 
 }  // namespace pa

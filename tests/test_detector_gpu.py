@@ -376,6 +376,8 @@ def test_fp16x3_entries_vgpr_weights(gold, B):
         y1, y1b = m(x), m(x)
         m.set_variants({6: 60})  # layer2 with deferred stores
         y3 = m(x)
+        m.set_variants({6: 62})  # layer3 with deferred stores
+        y4 = m(x)
         m.set_variants({6: 58})
         m.set_trace(buf)
         y2 = m(x)
@@ -384,6 +386,7 @@ def test_fp16x3_entries_vgpr_weights(gold, B):
         m.set_variants({})
     assert (y5 - y1).abs().max().item() * PX <= 1e-4
     assert torch.equal(y0, y1) and torch.equal(y1, y1b) and torch.equal(y1, y2) and torch.equal(y1, y3)
+    assert torch.equal(y1, y4)
     name, seed, xg = cases()[3]
     mg = model(seed, precision="fp16x3")
     try:
@@ -434,19 +437,23 @@ def test_split_k_reduce_forms_bit_identical(precision):
 def test_fp16x3_layer1_vgpr_weight_kernel_bit_identical(B):
     """fp16x3 layer1 on conv_x3v.hip (shipped: weights hi / lo in VGPRs, persistent 8-row tiles)
     sums its products in conv_gx X3's merged-step order (variant 1:91) and splits the same way:
-    bit-identical; so is its deferred-store form on the plain convs (1:92)."""
+    bit-identical; so are its plain convs with their stores at the tile end (1:90; shipped from round
+    6: deferred into the next tile's K loop)."""
     m = model(0, precision="fp16x3")
     x = torch.from_numpy(synth.synthetic_frames(5, B)).cuda()
     y0 = m(x)
     try:
         m.set_variants({1: 91})
         y1 = m(x)
-        m.set_variants({1: 92})
+        m.set_variants({1: 90})
         y2 = m(x)
+        m.set_variants({1: 98})  # the residual convs' stores deferred as well
+        y3 = m(x)
     finally:
         m.set_variants({})
     assert torch.equal(y0, y1)
     assert torch.equal(y0, y2)
+    assert torch.equal(y0, y3)
 
 
 def test_fp16x3_merged_steps_match_three_block_form(gold):
