@@ -79,7 +79,8 @@ struct C64v {
 // loop done to stores issued on the 16-row form, profiles/r06e trace).  Plain convs (RP): the
 // outputs are staged in the idle residual buffer of the tile (the residual tile's layout: 4 VGPRs
 // per store, read back just before it); residual convs: held in 16 VGPRs (pend).
-template <int EPI, int TH, int DBG = 0, bool DYN = false, bool DS = false>
+// ND (VGPR form): only the tile's last ND of its TM rows are deferred, the others stored at the tile end
+template <int EPI, int TH, int DBG = 0, bool DYN = false, bool DS = false, int ND = 4>
 __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntiles) {
   using G = C64v<TH>;
   constexpr int TW = G::TW, PW = G::PW, NP = G::NP, NWAVE = G::NWAVE, PXB = G::PXB, PJ = G::PJ;
@@ -258,8 +259,9 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   unsigned kdyn = 0;
   static_assert(!(DS && DYN), "deferred stores with static tiles");
   _Float16* __restrict__ out = (_Float16*)a.out;
-  constexpr bool DSL = DS && RP && !(EPI & EPI_RES);  // DS through LDS (the residual buffers are idle)
-  half8 pend[DSL ? 1 : TM];  // DS in VGPRs: the previous tile's outputs, rows 4 wm + tm
+  constexpr bool DSL = DS && RP && !(EPI & EPI_RES) && ND >= TM;  // DS through LDS (the residual buffers are idle)
+  constexpr int NDR = DSL ? TM : (ND < TM ? ND : TM);  // rows deferred: TM - NDR .. TM - 1
+  half8 pend[DSL ? 1 : NDR];  // DS in VGPRs: the previous tile's outputs, rows 4 wm + TM - NDR + i
   unsigned pend_base = 0;  // DS: their tile's byte offset (wave-uniform)
   // this lane's byte offset in a tile: row 4 wm (+ tm rows), column o, channels 32 wn + 8 q
   const unsigned olane = (unsigned)(((wm * 4 * W + o) * 64 + wn * 32 + q * 8) * 2);
@@ -318,8 +320,8 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
           dma_res(K - PDW, img, th0, tw0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (DS && K >= PDW + ((EPI & EPI_RES) ? RDW : 0) && K < PDW + ((EPI & EPI_RES) ? RDW : 0) + TM) {
-        constexpr int I = K - PDW - ((EPI & EPI_RES) ? RDW : 0);  // the previous tile's row I (issued last)
+      } else if constexpr (DS && K >= PDW + ((EPI & EPI_RES) ? RDW : 0) && K < PDW + ((EPI & EPI_RES) ? RDW : 0) + NDR) {
+        constexpr int I = K - PDW - ((EPI & EPI_RES) ? RDW : 0);  // the previous tile's row TM - NDR + I (issued last)
         __builtin_amdgcn_sched_barrier(0);
         if (t > 0) {
           if constexpr (DSL) {
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
             const half8 v = *reinterpret_cast<const half8*>(resb(buf ^ 1) + px * 128 + (((wn * 4 + q) ^ (px & 7)) << 4));
             store16<true>(out, pend_base + olane + I * orow, v);
           } else {
-            store16<true>(out, pend_base + olane + I * orow, pend[I]);
+            store16<true>(out, pend_base + olane + (TM - NDR + I) * orow, pend[I]);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
     // them, may stay in flight
     if constexpr (DS) {
       if (t > 0)
-        xwait_vm<TM>();
+        xwait_vm<NDR>();
       else
         xwait_vm<0>();
     } else {
@@ -371,7 +373,12 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
       if constexpr (DSL) {
         *reinterpret_cast<half8*>(resb(buf) + px * 128 + (((wn * 4 + q) ^ (px & 7)) << 4)) = hv;
       } else if constexpr (DS) {
-        pend[tm] = hv;
+        if (tm >= TM - NDR) {
+          pend[tm - (TM - NDR)] = hv;
+        } else {
+          const unsigned ob = (unsigned)((((img * H + th0 + wm * 4 + tm) * W + tw0 + o) * 64 + wn * 32 + q * 8) * 2);
+          store16<true>(out, ob, hv);
+        }
       } else {
         const unsigned ob = (unsigned)((((img * H + th0 + wm * 4 + tm) * W + tw0 + o) * 64 + wn * 32 + q * 8) * 2);
         store16<true>(out, ob, hv);
@@ -402,7 +409,7 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
         }
       } else {
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) store16<true>(out, pend_base + olane + tm * orow, pend[tm]);
+        for (int i = 0; i < NDR; ++i) store16<true>(out, pend_base + olane + (TM - NDR + i) * orow, pend[i]);
       }
     }
   }
@@ -418,7 +425,7 @@ __global__ __launch_bounds__(TH * 32, 2) void conv3x3_c64v(ConvArgs a, int ntile
   }
 }
 
-template <int TH, int DBG, bool DYN = false, bool DS = false>
+template <int TH, int DBG, bool DYN = false, bool DS = false, int ND = 4>
 static int run_c64v(const ConvArgs& a, hipStream_t s) {
   PA_CHECK(!DYN || a.cnt, "c64v conv: dynamic tiles need the handle's counters");
   PA_CHECK(a.Hout % TH == 0 && a.Wout % 16 == 0, "c64v conv: %dx%d not tiled by %dx16", a.Hout, a.Wout, TH);
@@ -431,9 +438,9 @@ static int run_c64v(const ConvArgs& a, hipStream_t s) {
     if (grid < 8) return run_c64v<TH, DBG, false>(a, s);
   }
   if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES, TH, DBG, DYN, DS>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU | EPI_RES, TH, DBG, DYN, DS, ND>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
   else
-    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU, TH, DBG, DYN, DS>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
+    hipLaunchKernelGGL((conv3x3_c64v<EPI_RELU, TH, DBG, DYN, DS, ND>), dim3(grid), dim3(TH * 32), 0, s, a, tiles);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }
@@ -458,6 +465,8 @@ int launch_conv3x3_c64v(const ConvArgs& a, int variant, hipStream_t s) {
   // 10: variant 2 with deferred stores (DS); 11 / 12: 16-row / 8-row DS with s_memrealtime stamps
   if (variant == 10) return (a.epi & EPI_RES) ? run_c64v<8, 0, false, true>(a, s) : run_c64v<16, 0, false, true>(a, s);
   if (variant == 13) return (a.epi & EPI_RES) ? run_c64v<8, 0>(a, s) : run_c64v<16, 0, false, true>(a, s);
+  // 15: the plain convs with their last row of 4 deferred in VGPRs (254; two rows spill), residual as shipped
+  if (variant == 15) return (a.epi & EPI_RES) ? run_c64v<8, 0>(a, s) : run_c64v<16, 0, false, true, 1>(a, s);
   if (variant == 11 && a.trace) return run_c64v<16, 4, false, true>(a, s);
   if (variant == 12 && a.trace) return run_c64v<8, 4, false, true>(a, s);
 #if PA_TIMING_VARIANTS

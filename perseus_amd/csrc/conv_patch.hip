@@ -450,6 +450,10 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
       if (kname) *kname = "conv3x3c64_l1";
       return launch_conv3x3_c64v(a, g_variant[1] - 83, s);
     }
+    if (l1 && g_variant[1] == 99) {  // conv_c64v.hip 15: the plain convs' last row deferred
+      if (kname) *kname = "conv3x3c64_l1";
+      return launch_conv3x3_c64v(a, 15, s);
+    }
     if (a.Hout == 64 && a.Cout == 64 && a.Cin == 64 && g_variant[1] >= 60 && g_variant[1] <= 69) {
       if (kname) *kname = "conv3x3c64_l1";
       return launch_conv3x3_c64d(a, g_variant[1] - 60, s);

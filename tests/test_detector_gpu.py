@@ -516,6 +516,7 @@ def test_kernel_variants_agree_bit_for_bit(B):
         (((1, 83),), y0),  # layer1: conv_c64v.hip 8-row tiles, tiles after the first from per-XCD counters
         (((1, 93),), y0),  # layer1: conv_c64v.hip with deferred stores (plain: staged in LDS, residual: in VGPRs)
         (((1, 96),), y0),  # layer1: deferred stores on the plain convs only
+        (((1, 99),), y0),  # layer1: the plain convs' last row deferred
         (((0, 30), (1, 69)), y0),  # stem bands in XCD-grouped order; conv_c64d tiles in the plain order (same arithmetic)
         (((6, 40),), y0),  # conv_s2w on layers 2 and 3 (round 5's entries) vs conv_s2v (layer2, weights in VGPRs)
         (((6, 48),), y0),  # layer2's entry with its stores at the tile end (shipped: deferred); layer4's in the 2 x 4 XCD split
