@@ -18,7 +18,7 @@ int launch_conv3x3s2_x3(const ConvS2Args& a, hipStream_t s, const char** kname) 
   // 6:57 / 6:58: layer2 on conv_x3s2v.hip, layer3 on conv_x3s2k.hip (58: with s_memrealtime stamps)
   // shipped from round 6: layer2 on conv_x3s2v.hip (44.6 vs 49.3 us on one box, 46.1 vs 45.7 on another:
   // profiles/r06h/ab.log, r06e/ab_x3.log; its minima 41-42 us against 45-49)
-  if ((v == 0 || v == 57 || v == 58) && a.Hout == 32 && a.Cin == 64 && a.wfrag)
+  if ((v == 0 || v == 57 || v == 58 || v == 62) && a.Hout == 32 && a.Cin == 64 && a.wfrag)
     return launch_conv3x3s2_v3(a, v == 58 ? 1 : 0, s, kname);
   // 6:60 / 6:61: layer2 on conv_x3s2v.hip with deferred stores (61: with stamps); layer3 as shipped
   if ((v == 60 || v == 61) && a.Hout == 32 && a.Cin == 64 && a.wfrag) return launch_conv3x3s2_v3(a, v == 60 ? 2 : 3, s, kname);
