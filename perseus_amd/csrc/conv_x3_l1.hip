@@ -3,7 +3,7 @@
 #include "conv_gx.h"
 
 namespace pa {
-int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds, bool dsr);
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds, bool dsr, int ndr);
 }
 
 namespace pa {
@@ -20,8 +20,11 @@ int launch_conv3x3_x3_l1(const ConvArgs& a, hipStream_t s) {
   // round 6: the plain convs with deferred stores (53.3 vs 56.9 us per launch, profiles/r06j/ab.log;
   // bit-identical); 1:90 keeps their stores at the tile end (1:92 = the shipped form); 1:98: the
   // residual convs' stores deferred as well (staged in place of their residual)
+  // shipped (round 6): the residual convs' last row deferred in VGPRs (56.3 / 57.2 vs 59.3 / 60.2 us
+  // per launch, profiles/r06m/ab_x3.log; bit-identical); 1:97 keeps all their stores at the tile end,
+  // 1:99 defers their last two rows (3 VGPRs spill)
   const int v = g_variant[1];
-  return launch_conv3x3_x3v(a, s, v != 90, v == 98);
+  return launch_conv3x3_x3v(a, s, v != 90, v == 98, v == 97 ? 0 : v == 99 ? 2 : 1);
 }
 
 }  // namespace pa

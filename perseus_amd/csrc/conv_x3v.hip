@@ -49,7 +49,8 @@ __device__ __forceinline__ int x3v_wswz(int row, int chunk) { return row * 256 +
 // read (its own 8 + 8 bytes of the tile's residual buffer); that buffer receives the tile-after-next's
 // residual in the next K loop, so there the residual DMAs move behind the staged reads and an LDS
 // barrier (steps 14 .. 17).
-template <int EPI, bool DS = false>
+// NDX < 4 (residual convs): only the tile's last NDX rows deferred, held in VGPRs (2 NDX half4)
+template <int EPI, bool DS = false, int NDX = 4>
 __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
   using namespace x3v;
   constexpr int TM = 4;
@@ -158,14 +159,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
   stage(xic<0>{}, xic<WR0>{});
   stage(xic<WR0>{}, xic<9>{});
 
-  constexpr bool DSR = DS && (EPI & EPI_RES);  // staged in the residual buffer
-  constexpr int RD0 = DSR ? PDW + 2 * TM : PDW;  // first residual-DMA step
+  constexpr bool DSR = DS && (EPI & EPI_RES) && NDX >= TM;  // staged in the residual buffer
+  constexpr int NDR = DS && !DSR && NDX < TM ? NDX : TM;    // rows deferred: TM - NDR .. TM - 1
+  constexpr int RD0 = DSR ? PDW + 2 * TM : PDW;             // first residual-DMA step
+  constexpr int SS = (DS && !DSR && (EPI & EPI_RES)) ? PDW + RDW : PDW;  // first deferred-store step
   _Float16* __restrict__ out = (_Float16*)a.out;
   // DSR: this lane's staged chunk of tile pixel px, plane pl (the residual read's address)
   auto stg_off = [&](int px, int pl) __attribute__((always_inline)) {
     return px * 256 + (((8 * pl + (c0 >> 3)) ^ (px & 15)) << 4) + (c0 & 4) * 2;
   };
-  half4 ph[DS && !DSR ? TM : 1], pl[DS && !DSR ? TM : 1];  // DS (plain): the previous tile's hi / lo outputs
+  half4 ph[DS && !DSR ? NDR : 1], pl[DS && !DSR ? NDR : 1];  // DS (VGPRs): the previous tile's hi / lo outputs
   int pend_base = 0;                        // DS: their tile's first element (wave-uniform)
   const int olane = ((wm * 4) * W + o) * 128 + c0;
   for (int t = 0; j < ntiles; ++t, j += gridDim.x) {
@@ -223,16 +226,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
         if constexpr (DSR && K == RD0) lds_barrier();  // every wave's staged reads of buf ^ 1 retired
         if (has_next) dma_res(K - RD0, onext.img, onext.h0 + 1, onext.x0 + 1, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (DS && K >= PDW && K < PDW + 2 * TM) {  // the previous tile's outputs, row (K - PDW) / 2
-        constexpr int I = K - PDW;
+      } else if constexpr (DS && K >= SS && K < SS + 2 * NDR) {  // the previous tile's row TM - NDR + (K - SS) / 2
+        constexpr int I = K - SS, R = TM - NDR + (I >> 1);
         __builtin_amdgcn_sched_barrier(0);
         if (t > 0) {
           half4 v;
           if constexpr (DSR)
-            v = *reinterpret_cast<const half4*>(smem + (buf ^ 1) * BSTR + PATCHB + stg_off((wm * 4 + (I >> 1)) * TW + o, I & 1));
+            v = *reinterpret_cast<const half4*>(smem + (buf ^ 1) * BSTR + PATCHB + stg_off((wm * 4 + R) * TW + o, I & 1));
           else
             v = (I & 1) ? pl[I >> 1] : ph[I >> 1];
-          *reinterpret_cast<half4*>(out + pend_base + olane + (I >> 1) * W * 128 + (I & 1) * 64) = v;
+          *reinterpret_cast<half4*>(out + pend_base + olane + R * W * 128 + (I & 1) * 64) = v;
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -242,7 +245,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
     // in flight (DSR: the residual DMAs come after them)
     if constexpr (DS && !DSR) {
       if (t > 0)
-        xwait_vm<2 * TM>();
+        xwait_vm<2 * NDR>();
       else
         xwait_vm<0>();
     } else {
@@ -272,9 +275,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
       if constexpr (DSR) {  // in place of this lane's residual chunk
         *reinterpret_cast<half4*>(smem + buf * BSTR + PATCHB + stg_off(px, 0)) = hv;
         *reinterpret_cast<half4*>(smem + buf * BSTR + PATCHB + stg_off(px, 1)) = lv;
-      } else if constexpr (DS) {
-        ph[tm] = hv;
-        pl[tm] = lv;
+      } else if (DS && tm >= TM - NDR) {
+        ph[DS ? tm - (TM - NDR) : 0] = hv;
+        pl[DS ? tm - (TM - NDR) : 0] = lv;
       } else {
         const size_t pix = ((size_t)img * H + th0 + wm * 4 + tm) * W + tw0 + o;
         *reinterpret_cast<half4*>(out + pix * 128 + c0) = hv;
@@ -288,14 +291,14 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
     if ((int)blockIdx.x < ntiles) {
       const int lb = ((ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x) & 1;  // the last tile's buffer
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
+      for (int tm = TM - NDR; tm < TM; ++tm) {
         half4 vh, vl;
         if constexpr (DSR) {
           vh = *reinterpret_cast<const half4*>(smem + lb * BSTR + PATCHB + stg_off((wm * 4 + tm) * TW + o, 0));
           vl = *reinterpret_cast<const half4*>(smem + lb * BSTR + PATCHB + stg_off((wm * 4 + tm) * TW + o, 1));
         } else {
-          vh = ph[tm];
-          vl = pl[tm];
+          vh = ph[tm - (TM - NDR)];
+          vl = pl[tm - (TM - NDR)];
         }
         *reinterpret_cast<half4*>(out + pend_base + olane + tm * W * 128) = vh;
         *reinterpret_cast<half4*>(out + pend_base + olane + tm * W * 128 + 64) = vl;
@@ -304,8 +307,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x3v(ConvArgs a, int ntiles) {
   }
 }
 
-// ds / dsr: the plain / residual convs with deferred stores (DS)
-int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds, bool dsr) {
+// ds / dsr: the plain / residual convs with deferred stores (DS); ndr = 1 / 2: the residual convs'
+// last 1 / 2 rows deferred in VGPRs
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds, bool dsr, int ndr) {
   PA_CHECK(a.Cin == 64 && a.Cout == 64 && a.stride == 1 && a.pad == 1 && a.Hin == a.Hout && a.Win == a.Wout,
            "x3v conv: Cin=Cout=64 stride-1 only");
   PA_CHECK(a.Hout % x3v::TH == 0 && a.Wout % x3v::TW == 0 && a.Wout <= 96, "x3v conv: %dx%d", a.Hout, a.Wout);
@@ -318,6 +322,10 @@ int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds, bool dsr) {
   const int grid = tiles < cus ? tiles : cus;
   if ((a.epi & EPI_RES) && dsr)
     hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU | EPI_RES, true>), dim3(grid), dim3(512), 0, s, a, tiles);
+  else if ((a.epi & EPI_RES) && ndr == 1)
+    hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU | EPI_RES, true, 1>), dim3(grid), dim3(512), 0, s, a, tiles);
+  else if ((a.epi & EPI_RES) && ndr == 2)
+    hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU | EPI_RES, true, 2>), dim3(grid), dim3(512), 0, s, a, tiles);
   else if (a.epi & EPI_RES)
     hipLaunchKernelGGL((conv3x3_x3v<EPI_RELU | EPI_RES>), dim3(grid), dim3(512), 0, s, a, tiles);
   else if (ds)
@@ -328,6 +336,6 @@ int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s, bool ds, bool dsr) {
   return PA_OK;
 }
 
-int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s) { return launch_conv3x3_x3v(a, s, false, false); }
+int launch_conv3x3_x3v(const ConvArgs& a, hipStream_t s) { return launch_conv3x3_x3v(a, s, false, false, 0); }
 
 }  // namespace pa

@@ -438,7 +438,8 @@ def test_fp16x3_layer1_vgpr_weight_kernel_bit_identical(B):
     """fp16x3 layer1 on conv_x3v.hip (shipped: weights hi / lo in VGPRs, persistent 8-row tiles)
     sums its products in conv_gx X3's merged-step order (variant 1:91) and splits the same way:
     bit-identical; so are its plain convs with their stores at the tile end (1:90; shipped from round
-    6: deferred into the next tile's K loop)."""
+    6: deferred into the next tile's K loop) and its residual convs with every store at the tile end
+    (1:97; shipped from round 6: the last row deferred)."""
     m = model(0, precision="fp16x3")
     x = torch.from_numpy(synth.synthetic_frames(5, B)).cuda()
     y0 = m(x)
@@ -449,11 +450,16 @@ def test_fp16x3_layer1_vgpr_weight_kernel_bit_identical(B):
         y2 = m(x)
         m.set_variants({1: 98})  # the residual convs' stores deferred as well
         y3 = m(x)
+        m.set_variants({1: 97})  # the residual convs' stores all at the tile end
+        y4 = m(x)
+        m.set_variants({1: 99})  # the residual convs' last two rows deferred (VGPRs)
+        y5 = m(x)
     finally:
         m.set_variants({})
     assert torch.equal(y0, y1)
     assert torch.equal(y0, y2)
     assert torch.equal(y0, y3)
+    assert torch.equal(y0, y4) and torch.equal(y0, y5)
 
 
 def test_fp16x3_merged_steps_match_three_block_form(gold):
