@@ -31,11 +31,17 @@ struct ConvL {
   size_t w_off;   // element offset into the packed weight arrays (w16 / w32)
   size_t b_off;   // element offset into the bias / scale arrays
   size_t w3_off;  // element offset into the fp16x3 weight planes (w3)
+  long wk_off = -1;  // layer2 3x3 s1 convs: element offset into pa_detector::wk2 (conv_s1k.hip order)
 };
 
 struct Block {
   int conv1, conv2, ds;  // indices into convs; ds = -1 when identity
 };
+
+// conv_gx.h xperm on the host (weight packing)
+static inline int xperm_host(int rho) { return (rho & ~31) | (((rho >> 2) & 3) << 3) | (((rho >> 4) & 1) << 2) | (rho & 3); }
+// layer2's 3x3 s1 convs with the weights in VGPRs (conv_s1k.hip)
+int launch_conv3x3_s1k(const ConvArgs& a, const _Float16* wk, int variant, hipStream_t s, const char** kname);
 
 }  // namespace pa
 
@@ -51,6 +57,7 @@ struct pa_detector {
   _Float16* wv4 = nullptr;
   _Float16* wv2x3 = nullptr;  // fp16x3 layer2 entry's hi / lo planes in conv_x3s2v.hip's register order
   _Float16* wv3x3 = nullptr;  // fp16x3 layer3 entry's in conv_x3s2k.hip's order
+  _Float16* wk2 = nullptr;    // layer2's three 3x3 s1 convs in conv_s1k.hip's register order
   _Float16* w3 = nullptr;   // fp16x3: per conv [cout][taps][hi (cin) | lo (cin)] of w * 2^e (stem: hi plane, lo plane)
   float* scl = nullptr;     // fp16x3: 2^-e per output channel (indexed like bias)
   float* bstem3 = nullptr;  // fp16x3 stem: bias * 2^e (the stem's accumulator starts from it)
@@ -237,6 +244,35 @@ static int build(pa_detector* d, const float* blob, size_t nfloats) {
     if (c.cin == 128 && c.cout == 256 && !d->wv3) rc = pack_vgpr(bk, 4, &d->wv3);
     if (c.cin == 256 && c.cout == 512 && !d->wv4) rc = pack_vgpr(bk, 2, &d->wv4);
     if (rc != PA_OK) return rc;
+  }
+  // layer2's 3x3 stride-1 convs (128 -> 128) in conv_s1k.hip's order: per conv [h 2][wb 2][wn 2]
+  // [fragment 18][tn 2][lane 64][8] of channel 64 h + xperm(32 wn + 16 tn + r16), input channels
+  // 64 wb + 32 (k & 1) + 8 q + e, tap k / 2
+  {
+    std::vector<_Float16> hv;
+    for (pa::ConvL& c : d->convs) {
+      if (c.cin != 128 || c.cout != 128 || c.ks != 3 || c.stride != 1) continue;
+      c.wk_off = (long)hv.size();
+      hv.resize(hv.size() + (size_t)2 * 2 * 2 * 18 * 2 * 64 * 8);
+      _Float16* dst = hv.data() + c.wk_off;
+      for (int hh = 0; hh < 2; ++hh)
+        for (int wb = 0; wb < 2; ++wb)
+          for (int wn = 0; wn < 2; ++wn)
+            for (int k = 0; k < 18; ++k)
+              for (int tn = 0; tn < 2; ++tn)
+                for (int lane = 0; lane < 64; ++lane)
+                  for (int e = 0; e < 8; ++e) {
+                    const int q = lane >> 4, r16 = lane & 15;
+                    const int co = 64 * hh + pa::xperm_host(32 * wn + 16 * tn + r16);
+                    const int ci = 64 * wb + 32 * (k & 1) + 8 * q + e;
+                    dst[((((((size_t)hh * 2 + wb) * 2 + wn) * 18 + k) * 2 + tn) * 64 + lane) * 8 + e] =
+                        h16[c.w_off + (size_t)co * 9 * 128 + (size_t)(k >> 1) * 128 + ci];
+                  }
+    }
+    if (!hv.empty()) {
+      PA_HIP(hipMalloc(&d->wk2, hv.size() * sizeof(_Float16)));
+      PA_HIP(hipMemcpy(d->wk2, hv.data(), hv.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
   }
   // the fp16x3 layer2 entry's hi / lo planes in conv_x3s2v.hip's register order: [wave 8][fragment
   // 20][plane 2][lane 64][8] of channel 16 wave + r16, input channels 32 (k & 1) + 8 q + e (fragment
@@ -437,10 +473,13 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   int launch = 1;  // stem = 0
   auto trace = [&]() { return g_trace ? g_trace + (size_t)TRACE_LAUNCH * launch++ : nullptr; };
   // stride-1 convs: split-K form for small batches (pa_detector_set_split_k, conv_splitk.hip)
-  auto conv_s1 = [&](ConvArgs& a, const char** kn) -> int {
+  auto conv_s1 = [&](ConvArgs& a, const char** kn, const ConvL& cl) -> int {
     if (!(a.epi & EPI_HEAD)) a.cnt = d->tctr;  // (only conv_c64v.hip reads it)
     if constexpr (std::is_same<T, _Float16>::value) {
       const int layer = a.Hout == 64 ? 1 : a.Hout == 32 ? 2 : a.Hout == 16 ? 3 : a.Hout == 8 ? 4 : 0;
+      // 2:80 - 2:82 (A/B): layer2 on conv_s1k.hip (weights in VGPRs, K split over the waves)
+      if (layer == 2 && g_variant[2] >= 80 && g_variant[2] <= 82 && d->wk2 && cl.wk_off >= 0)
+        return launch_conv3x3_s1k(a, d->wk2 + cl.wk_off, g_variant[2] - 80, s, kn);
       // g_variant[layer] == 71 (A/B): layer2 split as well, layer1 on the persistent kernel
       if (layer && small && (g_variant[layer] == 0 || g_variant[layer] == 71 || (g_variant[layer] >= 35 &&
                                                                                    g_variant[layer] <= 39)) &&
@@ -522,7 +561,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       a.epi = EPI_RELU;
       a.trace = trace();
       if (c1.stride == 1)
-        PA_RUN(conv_s1(a, &kn), kn);
+        PA_RUN(conv_s1(a, &kn, c1), kn);
       else
         PA_RUN(launch_conv<T>(a, 3, s, &kn), kn);
       if (b.ds >= 0) {
@@ -565,7 +604,7 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
       b2.fcb = d->fcb;
       b2.y = y;
     }
-    PA_RUN(conv_s1(b2, &kn), kn);
+    PA_RUN(conv_s1(b2, &kn, c2), kn);
     if (b.ds >= 0) std::swap(X, D);
     hw = ho;
   }
@@ -865,6 +904,7 @@ void pa_detector_destroy(pa_detector* d) {
   if (d->wv4) hipFree(d->wv4);
   if (d->wv2x3) hipFree(d->wv2x3);
   if (d->wv3x3) hipFree(d->wv3x3);
+  if (d->wk2) hipFree(d->wk2);
   hipFree(d->scl);
   hipFree(d->bstem3);
   if (d->ws) hipFree(d->ws);

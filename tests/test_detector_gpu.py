@@ -566,6 +566,32 @@ def test_s2k_entries_vgpr_weights_k_split(B):
     assert int((buf != 0).sum().item()) > 0  # the stamps were written
 
 
+@pytest.mark.parametrize("B", [1, 3, 64, 70])
+def test_s1k_layer2_vgpr_weights_k_split(B):
+    """Layer2's three 3x3 stride-1 convs on conv_s1k.hip (weights in VGPRs, the K sum split over the
+    waves by 64-channel input block, partials added in block order; variant 2:80): another f32
+    summation order than conv_gx.h, so within 0.05 px of it; its timestamping form (2:81) is
+    bit-identical; deterministic over repeats; odd batches (70: a partial round of tiles) included."""
+    m = model(0)
+    x = torch.from_numpy(synth.synthetic_frames(6, B)).cuda()
+    y0 = m(x)
+    buf = torch.zeros(24 * 65536, dtype=torch.int64, device="cuda")
+    try:
+        m.set_variants({2: 80})
+        y1 = m(x)
+        y1b = m(x)
+        m.set_variants({2: 81})
+        m.set_trace(buf)
+        y2 = m(x)
+    finally:
+        m.set_trace(None)
+        m.set_variants({})
+    assert (y0 - y1).abs().max().item() * PX <= 0.05
+    assert torch.equal(y1, y1b)
+    assert torch.equal(y1, y2)
+    assert int((buf != 0).sum().item()) > 0  # the stamps were written
+
+
 def test_forward_into_out_buffer():
     """forward(x, out=buf) writes the same keypoints into buf (bench.py's step) and rejects a bad buffer."""
     m = model(0)
