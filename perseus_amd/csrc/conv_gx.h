@@ -299,10 +299,21 @@ __device__ __forceinline__ HiLo split_x3(float v) {
 // most one workgroup.  (A fix-up in the same launch -- write-through partials, a per-tile
 // arrival counter, the last arriver summing -- measured slower than the separate reduce:
 // 15-19 us against 9 + 4.7 us at B = 3)
+//
+// KS = 2 (K split inside the workgroup): two groups of WM x WN waves; group kg takes
+// half-step kg (K 32 kg .. 32 kg + 31) of every step, so with the same 8 waves a wave's
+// tile is twice as tall (layer4: 64 px x 32 ch instead of 32 x 32, 0.75 fragment reads
+// per MFMA instead of 1.0; the LDS, not the MFMA, bounds that launch).
+// Fragments are read one whole step ahead.  At the end the groups swap the halves of
+// their tiles through LDS and each finishes TM / 2 rows as (group 0's sum) + (group 1's):
+// a different K order from KS = 1 (not bit-identical; within fp16 rounding).
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G, int EPI, int DBG = 0, int FD = 1,
-          bool WT = true, bool X3 = false, bool XM = false, int PART = 0>
-__global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
-  constexpr int NW = WM * WN, NT = NW * 64;
+          bool WT = true, bool X3 = false, bool XM = false, int PART = 0, int KS = 1>
+__global__ __launch_bounds__(WM * WN * KS * 64) void conv3x3_gx(ConvArgs a, int xg) {
+  constexpr int NWG = WM * WN;  // waves per K group
+  constexpr int NW = NWG * KS, NT = NW * 64;
+  static_assert(KS == 1 || (KS == 2 && FD == 1 && !PART && !(EPI & EPI_HEAD) && (DBG == 0 || DBG == 4)),
+                "K split: fragments a step ahead, full epilogue");
   constexpr int NCB = CIN / 64;
   static_assert(!XM || (X3 && FD == 1), "merged X3 steps: fp16x3, fragments half a step ahead");
   static_assert(!PART || EPI == 0, "split-K partials: no epilogue");
@@ -321,6 +332,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   constexpr int BM = NI * TH * TW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int TME = TM / KS;  // 16-pixel rows a wave finishes in the epilogue
+  static_assert(TM % KS == 0, "K split: whole rows per group");
   static_assert(BN * 8 % NT == 0 && WDMA >= 1, "weight tile / threads");
   static_assert(WTM % 16 == 0 && WTN % 32 == 0, "wave tile");
   static_assert(TW >= 16 || (TW == 8 && NI == 2), "fragment geometry");
@@ -328,7 +341,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   // slot (t + PD) % NSLOT, written at step t, was last read by step t + PD - NSLOT,
   // which must lie before the last barrier: t - G with a barrier every G steps
   constexpr int NSLOT = PD + G;
-  constexpr int RL = PART ? 0 : XS * TN + ((EPI & EPI_RES) ? XS * TM * TN / 2 : 0);
+  constexpr int RL = PART ? 0 : XS * TN + ((EPI & EPI_RES) ? XS * TME * TN / 2 : 0);
   // epilogue loads (bias, residual) issued RSD steps before the end: early enough to
   // land, late enough not to hold their VGPRs across the whole K loop
   constexpr int RSD = NSTEPS >= 28 ? NSTEPS / 7 : 4;  // ~2 us before the end (layer4: 10 of 72 steps)
@@ -340,7 +353,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   char* wring = smem + 2 * PATCHB;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int kg = KS > 1 ? wid / NWG : 0, wl = wid - kg * NWG;  // K group, wave within it
+  const int wm = wl / WN, wn = wl - (wl / WN) * WN;
   const int q = lane >> 4, r16 = lane & 15;
   const int H = a.Hout, W = a.Wout;
   // PART: pixel stride and weight tap stride are the full conv's a.Cin; split blockIdx.y
@@ -435,10 +449,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
 
   const _Float16* __restrict__ res = (const _Float16*)a.res;
   _Float16* __restrict__ out = (_Float16*)a.out;
-  size_t pixo[TM];
-  bool ok[TM];
+  size_t pixo[TME];  // the epilogue's rows: tm = kg * TME + j
+  bool ok[TME];
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
+  for (int j = 0; j < TME; ++j) {
+    const int tm = kg * TME + j;
     const int mb = wm * WTM + tm * 16;
     int img, y, x;
     if constexpr (TW == 8) {
@@ -451,11 +466,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
       x = mb % TW + o;
     }
     const int n = img0 + img;
-    ok[tm] = n < a.B;
-    pixo[tm] = ((((size_t)(ok[tm] ? n : 0)) * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
+    ok[j] = n < a.B;
+    pixo[j] = ((((size_t)(ok[j] ? n : 0)) * H + th0 + y) * W + tw0 + x) * (XS * Cout) + n0 + wn * WTN + q * 8;
   }
-  half8 rv[TM][TN / 2];
-  half8 rl[X3 ? TM : 1][TN / 2];  // X3: the residual's lo plane
+  half8 rv[TME][TN / 2];
+  half8 rl[X3 ? TME : 1][TN / 2];  // X3: the residual's lo plane
   f32x4 bias[TN];
   f32x4 scl[X3 ? TN : 1];  // X3: 2^-e per output channel
   auto load_epi = [&]() __attribute__((always_inline)) {
@@ -467,7 +482,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     }
     if constexpr (EPI & EPI_RES) {
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
+      for (int tm = 0; tm < TME; ++tm)
 #pragma unroll
         for (int p = 0; p < TN / 2; ++p) {
           rv[tm][p] = *reinterpret_cast<const half8*>(res + pixo[tm] + p * 32);
@@ -534,6 +549,69 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
   };
   // step s + 1's data landed before the barrier that closed step s - 1, so with
   // FD = 2 both its halves are read during step s
+  // KS = 2: the fragments of step S (this group's half-step kg) into set S & 1
+  auto read_frags_k = [&](auto sc) __attribute__((always_inline)) {
+    constexpr int S = decltype(sc)::value;
+    constexpr int CB = S / 9, TAP = S % 9, SET = S & 1;
+    constexpr int TOFF = (TAP / 3) * PW + (TAP % 3);
+    const char* pb = patch + (CB & 1) * PATCHB;
+    const char* wb = wring + (S % NSLOT) * WSLOT;
+    const int ch = kg * 4 + q;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) fa[SET][tn] = *reinterpret_cast<const xu4*>(wb + xswz(wn * WTN + tn * 16 + r16, ch));
+    if constexpr (VB::two(CB))
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        fa2[SET][tn] = *reinterpret_cast<const xu4*>(wb + WB + xswz(wn * WTN + tn * 16 + r16, ch));
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) fb[SET][tm] = *reinterpret_cast<const xu4*>(pb + xswz(ppix[tm] + TOFF, ch));
+  };
+  // KS = 2: rows [T0, T1) of step S's MFMAs (XM: x_hi w_lo after x_hi w_hi, as mfma())
+  auto mfma_k = [&](auto sc, auto t0, auto t1) __attribute__((always_inline)) {
+    constexpr int S = decltype(sc)::value, SET = S & 1;
+    constexpr int T0 = decltype(t0)::value, T1 = decltype(t1)::value;
+#pragma unroll
+    for (int tm = T0; tm < T1; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa[SET][tn]),
+                                                             __builtin_bit_cast(half8, fb[SET][tm]), acc[tm][tn], 0, 0, 0);
+    if constexpr (VB::two(S / 9))
+#pragma unroll
+      for (int tm = T0; tm < T1; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, fa2[SET][tn]),
+                                                               __builtin_bit_cast(half8, fb[SET][tm]), acc[tm][tn], 0, 0, 0);
+  };
+  if constexpr (KS == 2) {
+    read_frags_k(xic<0>{});
+    gx_for<0, NSTEPS>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int S = decltype(sc)::value;
+      constexpr int CB = S / 9;
+      // step S + 1's data landed before the barrier that closed step S - 1 (as FD = 2)
+      if constexpr (S + 1 < NSTEPS) read_frags_k(xic<S + 1>{});
+      __builtin_amdgcn_s_setprio(1);
+      mfma_k(sc, xic<0>{}, xic<TM / 2>{});
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (S + PD < NSTEPS) dma_w(S + PD);
+      if constexpr (CB + 1 < VB::NVB && S == plan.ps(CB + 1)) dma_patch(CB + 1, (CB + 1) & 1);
+      if constexpr (S == plan.rs) {
+        __builtin_amdgcn_sched_barrier(0);
+        load_epi();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      mfma_k(sc, xic<TM / 2>{}, xic<TM>{});
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr ((S + 1) % G == 0 && S + 2 < NSTEPS) {
+        constexpr int V = S + G + 1 < NSTEPS ? S + G + 1 : NSTEPS - 1;
+        xwait_vm<plan.vm_after(S, V)>();
+        __builtin_amdgcn_s_barrier();
+      }
+    });
+  } else {
   read_frags(xic<0>{});
   if constexpr (FD == 2) read_frags(xic<1>{});
   gx_for<0, (DBG == 3 ? 0 : NSTEPS)>([&](auto sc) __attribute__((always_inline)) {
@@ -567,9 +645,40 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
       __builtin_amdgcn_s_barrier();
     }
   });
+  }
   if constexpr (DBG == 3) load_epi();
   if constexpr (DBG == 4) trace_stamp(a.trace, 2);
   xwait_vm<0>();  // bias / residual (also waited for by the compiler at their use)
+
+  // ae[j]: the finished sums of epilogue row kg * TME + j
+  f32x4 ae[TME][TN];
+  if constexpr (KS == 2) {
+    // every wave is past its last fragment read and its DMAs have landed (vmcnt(0)):
+    // the patch buffers take the swap; group kg hands over the rows the other finishes
+    static_assert(2 * NWG * TME * TN * 1024 <= 2 * PATCHB + NSLOT * WSLOT, "K split swap buffer");
+    f32x4* xb = reinterpret_cast<f32x4*>(smem);
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int j = 0; j < TME; ++j)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        xb[(((kg * NWG + wl) * TME + j) * TN + tn) * 64 + lane] = kg ? acc[j][tn] : acc[TME + j][tn];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int j = 0; j < TME; ++j)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const f32x4 o = xb[((((1 - kg) * NWG + wl) * TME + j) * TN + tn) * 64 + lane];
+        const f32x4 m = kg ? acc[TME + j][tn] : acc[j][tn];
+        ae[j][tn] = kg ? o + m : m + o;  // group 0's partial + group 1's
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < TME; ++j)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) ae[j][tn] = acc[j][tn];
+  }
 
   if constexpr (EPI & EPI_HEAD) {
     gx_head<TH, TW, NI, BN, NT, WTM, WTN, TM, TN, EPI>(a, smem, acc, bias, rv, img0, n0, ntn, o);
@@ -590,7 +699,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
     return;
   }
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
+  for (int tm = 0; tm < TME; ++tm) {
     if (!ok[tm]) continue;
 #pragma unroll
     for (int p = 0; p < TN / 2; ++p) {
@@ -599,13 +708,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv3x3_gx(ConvArgs a, int xg) {
       for (int j = 0; j < 8; ++j) {
         const int tn = 2 * p + (j >> 2), e = j & 3;
         if constexpr (X3) {
-          float v = acc[tm][tn][e] * scl[tn][e] + bias[tn][e];  // exact unscale (power of 2)
+          float v = ae[tm][tn][e] * scl[tn][e] + bias[tn][e];  // exact unscale (power of 2)
           if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j] + (float)rl[tm][p][j];
           const HiLo hl = split_x3(fmaxf(v, 0.f));
           hv[j] = hl.hi;
           lv[j] = hl.lo;
         } else {
-          float v = acc[tm][tn][e] + bias[tn][e];
+          float v = ae[tm][tn][e] + bias[tn][e];
           if constexpr (EPI & EPI_RES) v += (float)rv[tm][p][j];
           hv[j] = (_Float16)fmaxf(v, 0.f);
         }
@@ -636,7 +745,7 @@ static int run_gx_part(const ConvArgs& a, hipStream_t s) {
 }
 
 template <int TH, int TW, int NI, int BN, int WM, int WN, int CIN, int PD, int G = 1, int DBG = 0, int FD = 1,
-          bool WT = true, bool X3 = false, bool XM = false>
+          bool WT = true, bool X3 = false, bool XM = false, int KS = 1>
 static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
   PA_CHECK(a.epi == EPI_RELU || a.epi == (EPI_RELU | EPI_RES) || a.epi == (EPI_RELU | EPI_RES | EPI_HEAD),
            "gx conv: epilogue %d", a.epi);
@@ -652,7 +761,7 @@ static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
   PA_CHECK(!WT || (size_t)a.B * a.Hout * a.Wout * a.Cout * 2 * (X3 ? 2 : 1) < 0x7fffffffu, "gx conv: output over 2 GB");
   PA_CHECK(!X3 || (a.scale && !(a.epi & EPI_HEAD)), "gx conv (fp16x3): scale required, no fused head");
   if (a.epi & EPI_HEAD) {
-    if constexpr (TH == 8 && TW == 8 && NI == 2 && BN == 64 && WM * WN == 8 && DBG == 0 && !X3) {
+    if constexpr (TH == 8 && TW == 8 && NI == 2 && BN == 64 && WM * WN == 8 && DBG == 0 && !X3 && KS == 1) {
       PA_CHECK(a.pool && a.cnt && a.fcw && a.fcb && a.y && a.Cout == 512, "gx conv: fused head arguments");
       hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES | EPI_HEAD, DBG, FD, WT>),
                          dim3(tiles), dim3(WM * WN * 64), 0, s, a, x);
@@ -660,11 +769,11 @@ static int run_gx(const ConvArgs& a, int xg, hipStream_t s) {
       PA_CHECK(false, "gx conv: fused head needs the 2 x 8x8 x 64-channel tile");
     }
   } else if (a.epi & EPI_RES)
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT, X3, XM>),
-                       dim3(tiles), dim3(WM * WN * 64), 0, s, a, x);
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU | EPI_RES, DBG, FD, WT, X3, XM, 0, KS>),
+                       dim3(tiles), dim3(WM * WN * KS * 64), 0, s, a, x);
   else
-    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT, X3, XM>), dim3(tiles),
-                       dim3(WM * WN * 64), 0, s, a, x);
+    hipLaunchKernelGGL((conv3x3_gx<TH, TW, NI, BN, WM, WN, CIN, PD, G, EPI_RELU, DBG, FD, WT, X3, XM, 0, KS>),
+                       dim3(tiles), dim3(WM * WN * KS * 64), 0, s, a, x);
   PA_LAUNCH_CHECK();
   return PA_OK;
 }

@@ -19,6 +19,8 @@ int launch_conv3x3_gx_l3(const ConvArgs& a, int variant, hipStream_t s) {
   if (variant == 11) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 5>(a, xg, s);
   if (variant == 12) return run_gx<16, 16, 1, 64, 4, 2, 256, 3, 1, 6>(a, xg, s);
 #endif
+  // 16 (3:66): K split over two 4-wave groups (conv_gx.h KS = 2), 64 x 64 wave tiles
+  if (variant == 16) return run_gx<16, 16, 1, 64, 4, 1, 256, 3, 1, 0, 1, true, false, false, 2>(a, xg, s);
   switch (variant & 3) {
       case 1: return run_gx<8, 16, 1, 64, 2, 2, 256, 3>(a, xg, s);  // 80 KB LDS: 2 workgroups per CU
       case 2: return run_gx<16, 16, 1, 64, 4, 2, 256, 4, 3>(a, xg, s);

@@ -21,6 +21,9 @@ int launch_conv3x3_gx_l4(const ConvArgs& a, int variant, hipStream_t s) {
   if (variant == 13) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 2>(a, xgv_of(xg), s);
   if (variant == 14) return run_gx<8, 8, 2, 64, 4, 2, 512, 4, 1, 3>(a, xgv_of(xg), s);
 #endif
+  // 16 / 17 (4:66 / 4:67): K split over two 4-wave groups (conv_gx.h KS = 2), 64 x 32 wave tiles
+  if (variant == 16) return run_gx<8, 8, 2, 64, 2, 2, 512, 4, 1, 0, 1, true, false, false, 2>(a, 4, s);
+  if (variant == 17) return run_gx<8, 8, 2, 64, 2, 2, 512, 4, 2, 0, 1, true, false, false, 2>(a, 4, s);
   if (variant == 8 || variant == 9)  // 2-D XCD split: 4 / 2 channel groups per XCD
     return run_gx<8, 8, 2, 64, 4, 2, 512, 4>(a, variant == 8 ? 4 : 2, s);
   // shipped: 4 channel groups per XCD (round 2: HBM traffic 31-35 MB vs 46-51 per launch with the 1-D order,
