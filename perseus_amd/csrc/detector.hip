@@ -452,10 +452,11 @@ static int forward_t(pa_detector* d, const float* x, int B, float* y, hipStream_
   T* D = Tb + act_el;
   // g_variant[7] == 3: avgpool + fc fused into layer4's last conv (conv_gx.h gx_head).
   // Bit-identical to the separate head_fp16 and measured neutral (27.3 us for the fused
-  // launch vs 19.5 + 6.7 us; 176.7k vs 177.3k frames/s interleaved), so not shipped.
+  // launch vs 19.5 + 6.7 us; 176.7k vs 177.3k frames/s interleaved), so not shipped.  It runs
+  // with layer4 on its one-K-group form (4:65; the shipped K split has no fused head).
   bool fuse_head = false;
   if constexpr (std::is_same<T, _Float16>::value)
-    fuse_head = g_variant[7] == 3 && g_variant[4] == 0 && d->n_kp == 8 && d->H == 256 && d->W == 256 &&
+    fuse_head = g_variant[7] == 3 && g_variant[4] == 65 && d->n_kp == 8 && d->H == 256 && d->W == 256 &&
                 d->blocks.back().ds < 0;
   if (prof) prof->mark("start");
   const ConvL& st = d->convs[0];

@@ -505,13 +505,16 @@ def test_kernel_variants_agree_bit_for_bit(B):
             m.set_variants({})
 
     y0 = m(x)
+    y65 = run({4: 65})  # layer4 in one K group of 8 waves (shipped until round 6)
+    assert (y0 - y65).abs().max().item() * PX <= 0.05
     ys2x = run({6: 10})
     assert (y0 - ys2x).abs().max().item() * PX <= 0.05
     sets = (
-        (((1, 3), (2, 1), (3, 1), (4, 1), (0, 10)), y0),
+        (((1, 3), (2, 1), (3, 1), (4, 1), (0, 10)), y65),  # 4:1 = 4:65 with a barrier every 2 steps
         (((1, 30), (7, 1)), y0),  # layer1: register-staged kernel on every conv; the generic head
         (((1, 32),), y0),  # layer1: the one-tile patch kernel (independent of the shipped LDS-DMA kernel)
-        (((7, 3),), y0),  # avgpool + fc fused into layer4's last conv instead of head_fp16
+        (((7, 3), (4, 65)), y65),  # avgpool + fc fused into layer4's last conv instead of head_fp16
+        (((4, 67),), y0),  # layer4: the shipped K split named explicitly
         (((0, 16),), y0),  # stem: version 3 (every wave convolves and moves rows) vs the shipped role split
         (((0, 31),), y0),  # stem: bias as the first MFMA's accumulator input (BR) alone
         (((0, 33),), y0),  # stem: IL alone
@@ -590,6 +593,42 @@ def test_s1k_layer2_vgpr_weights_k_split(B):
     assert torch.equal(y1, y1b)
     assert torch.equal(y1, y2)
     assert int((buf != 0).sum().item()) > 0  # the stamps were written
+
+
+@pytest.mark.parametrize("B", [1, 3, 64, 70])
+def test_gx_k_split_variants(B):
+    """conv_gx.h's K split over two wave groups (KS = 2: group kg sums half-step kg of every step,
+    the groups swap tile halves through LDS and finish (group 0's partial) + (group 1's)), shipped on
+    layer4's 3x3 s1 convs in fp16 and fp16x3 (round 6), against the one-K-group forms shipped before
+    (4:65, fp16x3 4:74), and on layer3 (3:66, not shipped).  Another f32 summation order, so within
+    0.05 px in fp16 and 1e-4 px in fp16x3 (whose own error vs the f64 oracle is ~7e-5 px); every form
+    deterministic; the shipped fp16x3 within 1e-3 px of the f64 oracle; odd batches (a half-filled
+    image pair on layer4) included."""
+    x = torch.from_numpy(synth.synthetic_frames(6, B)).cuda()
+    m = model(0)
+    y0 = m(x)
+    assert torch.equal(y0, m(x))
+    try:
+        for v in ({3: 66}, {4: 65}):
+            m.set_variants(v)
+            y1 = m(x)
+            assert torch.equal(y1, m(x)), v
+            assert (y0 - y1).abs().max().item() * PX <= 0.05, v
+    finally:
+        m.set_variants({})
+    m3 = model(0, precision="fp16x3")
+    z0 = m3(x)
+    assert torch.equal(z0, m3(x))
+    try:
+        for v in ({4: 74}, {4: 72}):
+            m3.set_variants(v)
+            z1 = m3(x)
+            assert torch.equal(z1, m3(x)), v
+            assert (z0 - z1).abs().max().item() * PX <= (0.0 if v[4] == 72 else 1e-4), v
+    finally:
+        m3.set_variants({})
+    y64 = R.run(synth.synthetic_state_dict(0), synth.synthetic_frames(6, B), torch.float64)
+    assert np.abs(z0.cpu().numpy() - y64).max() * PX <= FP32_PX_MAX
 
 
 def test_forward_into_out_buffer():
