@@ -79,7 +79,10 @@ def _flags_digest() -> str:
     object (mtimes alone would link stale objects built with the old flags)."""
     import hashlib
 
-    return hashlib.sha256(repr((HIPCC, FLAGS, ARCH, CXX, HOST_FLAGS, sorted(EXTRA.items()))).encode()).hexdigest()
+    # the include path names this checkout's location: digest it relative to the tree, so the
+    # library built here counts as up to date in a copy of the tree elsewhere (the GPU box)
+    host = [f.replace(ROOT, "<root>") for f in HOST_FLAGS]
+    return hashlib.sha256(repr((HIPCC, FLAGS, ARCH, CXX, host, sorted(EXTRA.items()))).encode()).hexdigest()
 
 
 def _stamp_ok() -> bool:

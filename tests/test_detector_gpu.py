@@ -314,7 +314,7 @@ def test_profile_reports_every_kernel():
     assert names[5].startswith("conv3x3s2")
     assert torch.equal(y, m(x))
     try:
-        m.set_variants({7: 3})  # avgpool + fc fused into layer4's last conv
+        m.set_variants({7: 3, 4: 65})  # avgpool + fc fused into layer4's last conv (one-K-group form)
         names_fused = [n for n, _ in m.profile(x)[0]]
     finally:
         m.set_variants({})
@@ -653,9 +653,10 @@ def test_fused_head_repeats_and_batch_changes():
     m = model(1)
     for B in (2, 5, 64, 7, 130):
         x = torch.from_numpy(synth.synthetic_frames(3, B)).cuda()
-        ref = m(x)
         try:
-            m.set_variants({7: 3})
+            m.set_variants({4: 65})  # layer4 in one K group: the form the fused head extends
+            ref = m(x)
+            m.set_variants({7: 3, 4: 65})
             ys = [m(x) for _ in range(3)]
         finally:
             m.set_variants({})
