@@ -418,7 +418,9 @@ int launch_conv3x3_s1(const ConvArgs& a, hipStream_t s, const char** kname) {
     if (layer >= 2 && (g_variant[layer] == 0 || (g_variant[layer] >= 50 && g_variant[layer] <= 69))) {
       static const char* names[5] = {"", "conv3x3x_l1", "conv3x3x_l2", "conv3x3x_l3", "conv3x3x_l4"};
       if (kname) *kname = (a.epi & EPI_HEAD) ? "conv3x3x_l4_avgpool_fc" : names[layer];
-      const int v = g_variant[layer] == 0 ? 0 : g_variant[layer] - 50;
+      // layer4 ships its one-K-group form (conv_gx_l4.hip 15): the K split (0 / 17 there) is faster
+      // per launch back to back but 1.4 % slower over whole forwards (profiles/r06t/fwdab.log)
+      const int v = g_variant[layer] == 0 ? (layer == 4 ? 15 : 0) : g_variant[layer] - 50;
       if (a.Cin == 128 && a.Hout == 32) return launch_conv3x3_gx_l2(a, v, s);
       if (a.Cin == 256 && a.Hout == 16) return launch_conv3x3_gx_l3(a, v, s);
       if (a.Cin == 512 && a.Hout == 8) return launch_conv3x3_gx_l4(a, v, s);
